@@ -1,0 +1,195 @@
+"""Model and engine configuration.
+
+The reference serves ``meta-llama/Llama-3.1-8B-Instruct`` through vLLM with the knobs in
+infra/docker-compose.yml:16-27 (dtype float16, max_num_seqs 12, max_num_batched_tokens
+8192, gpu_memory_utilization 0.90, max_model_len 4096) and KV blocks of 16 tokens
+(llm/serve_llm.py:325).  ``EngineConfig`` keeps those names and defaults; the MI355X
+specific additions (tensor/data parallel degree, hipGraph buckets, decode partitioning)
+default to values sized for 288 GB of HBM3E per GPU.
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import asdict, dataclass, field, replace
+from pathlib import Path
+
+LLAMA3_ROPE_SCALING = {
+    "rope_type": "llama3",
+    "factor": 8.0,
+    "low_freq_factor": 1.0,
+    "high_freq_factor": 4.0,
+    "original_max_position_embeddings": 8192,
+}
+
+
+@dataclass(frozen=True)
+class ModelConfig:
+    name: str = "llama-3.1-8b"
+    vocab_size: int = 128256
+    hidden_size: int = 4096
+    intermediate_size: int = 14336
+    num_layers: int = 32
+    num_heads: int = 32
+    num_kv_heads: int = 8
+    head_dim: int = 128
+    rms_norm_eps: float = 1e-5
+    rope_theta: float = 500000.0
+    rope_scaling: dict | None = field(default_factory=lambda: dict(LLAMA3_ROPE_SCALING))
+    max_position_embeddings: int = 131072
+    tie_word_embeddings: bool = False
+    bos_token_id: int = 128000
+    eos_token_ids: tuple = (128001, 128008, 128009)
+
+    @property
+    def q_size(self) -> int:
+        return self.num_heads * self.head_dim
+
+    @property
+    def kv_size(self) -> int:
+        return self.num_kv_heads * self.head_dim
+
+    def num_params(self) -> int:
+        h, i, v = self.hidden_size, self.intermediate_size, self.vocab_size
+        per_layer = h * (self.q_size + 2 * self.kv_size) + self.q_size * h + 3 * h * i + 2 * h
+        emb = v * h * (1 if self.tie_word_embeddings else 2)
+        return self.num_layers * per_layer + emb + h
+
+    def kv_bytes_per_token(self, dtype_bytes: int = 2) -> int:
+        return self.num_layers * 2 * self.num_kv_heads * self.head_dim * dtype_bytes
+
+
+MODEL_PRESETS: dict[str, ModelConfig] = {
+    "llama-3.1-8b": ModelConfig(),
+    "llama-3-8b": ModelConfig(name="llama-3-8b", rope_scaling=None, max_position_embeddings=8192,
+                              eos_token_ids=(128001, 128009)),
+    "llama-3-70b": ModelConfig(name="llama-3-70b", hidden_size=8192, intermediate_size=28672,
+                               num_layers=80, num_heads=64, num_kv_heads=8, rope_scaling=None,
+                               max_position_embeddings=8192, eos_token_ids=(128001, 128009)),
+    "llama-3.1-70b": ModelConfig(name="llama-3.1-70b", hidden_size=8192, intermediate_size=28672,
+                                 num_layers=80, num_heads=64, num_kv_heads=8),
+    "llama-3.2-3b": ModelConfig(name="llama-3.2-3b", hidden_size=3072, intermediate_size=8192,
+                                num_layers=28, num_heads=24, num_kv_heads=8,
+                                tie_word_embeddings=True,
+                                rope_scaling=dict(LLAMA3_ROPE_SCALING, factor=32.0)),
+    "llama-3.2-1b": ModelConfig(name="llama-3.2-1b", hidden_size=2048, intermediate_size=8192,
+                                num_layers=16, num_heads=32, num_kv_heads=8, head_dim=64,
+                                tie_word_embeddings=True,
+                                rope_scaling=dict(LLAMA3_ROPE_SCALING, factor=32.0)),
+    # small shapes for tests / CPU plumbing runs (head_dim 128 like every Llama-3 >= 3B)
+    "tiny": ModelConfig(name="tiny", vocab_size=4096, hidden_size=256, intermediate_size=512,
+                        num_layers=2, num_heads=4, num_kv_heads=2, max_position_embeddings=4096,
+                        bos_token_id=3840, eos_token_ids=(3841, 3849)),
+    "small": ModelConfig(name="small", vocab_size=32768, hidden_size=1024, intermediate_size=2816,
+                         num_layers=4, num_heads=8, num_kv_heads=2, max_position_embeddings=8192,
+                         bos_token_id=32512, eos_token_ids=(32513, 32521)),
+}
+
+
+def resolve_model(model: str) -> tuple[ModelConfig, str | None]:
+    """Map a reference-style model id (``meta-llama/Llama-3.1-8B-Instruct``), a preset name
+    or a local HF directory (config.json [+ *.safetensors]) to a ModelConfig.
+    Returns (config, weights_dir or None)."""
+    p = Path(model)
+    if p.is_dir() and (p / "config.json").exists():
+        return config_from_hf(p / "config.json"), str(p)
+    key = model.lower().split("/")[-1]
+    if key in MODEL_PRESETS:
+        return MODEL_PRESETS[key], None
+    for k in ("3.1-70b", "3.2-3b", "3.2-1b", "3-70b", "3.1-8b", "3-8b"):
+        if k in key:
+            name = "llama-" + k
+            return MODEL_PRESETS[name], None
+    if "70b" in key:
+        return MODEL_PRESETS["llama-3-70b"], None
+    if "opt-125m" in key or "tiny" in key:
+        return MODEL_PRESETS["tiny"], None
+    return MODEL_PRESETS["llama-3.1-8b"], None
+
+
+def config_from_hf(path: Path) -> ModelConfig:
+    c = json.loads(Path(path).read_text())
+    eos = c.get("eos_token_id", 128009)
+    eos = tuple(eos) if isinstance(eos, list) else (eos,)
+    hd = c.get("head_dim") or c["hidden_size"] // c["num_attention_heads"]
+    return ModelConfig(
+        name=c.get("_name_or_path", Path(path).parent.name) or "hf-model",
+        vocab_size=c["vocab_size"], hidden_size=c["hidden_size"],
+        intermediate_size=c["intermediate_size"], num_layers=c["num_hidden_layers"],
+        num_heads=c["num_attention_heads"],
+        num_kv_heads=c.get("num_key_value_heads", c["num_attention_heads"]), head_dim=hd,
+        rms_norm_eps=c.get("rms_norm_eps", 1e-5), rope_theta=c.get("rope_theta", 10000.0),
+        rope_scaling=c.get("rope_scaling"),
+        max_position_embeddings=c.get("max_position_embeddings", 8192),
+        tie_word_embeddings=c.get("tie_word_embeddings", False),
+        bos_token_id=c.get("bos_token_id", 128000), eos_token_ids=eos)
+
+
+def _env_int(name, default):
+    v = os.environ.get(name)
+    try:
+        return int(v) if v not in (None, "") else default
+    except ValueError:
+        return default
+
+
+@dataclass
+class EngineConfig:
+    model: str = "meta-llama/Llama-3.1-8B-Instruct"
+    dtype: str = "bfloat16"              # reference default float16; both supported
+    max_model_len: int = 4096
+    max_num_seqs: int = 12
+    max_num_batched_tokens: int = 8192
+    gpu_memory_utilization: float = 0.90
+    block_size: int = 16                 # VLLM_BLOCK_SIZE default (serve_llm.py:325)
+    enable_prefix_caching: bool = True
+    tensor_parallel_size: int = 1
+    seed: int = 0
+    device: str = "cuda"
+    # hipGraph capture of decode steps (padded batch buckets)
+    use_graphs: bool = True
+    graph_batch_sizes: tuple = (1, 2, 4, 8, 16, 32, 64, 128, 256)
+    # decode split-K partition size (tokens) for the paged attention kernel
+    decode_partition_tokens: int = 256
+    # chunked prefill: max prompt tokens of one sequence per step (0 = max_num_batched_tokens)
+    long_prefill_token_threshold: int = 0
+    # fused native decode path (GEMV kernels) when available
+    fused_decode: bool = True
+    num_kv_blocks: int = 0               # 0 = size from gpu_memory_utilization
+    load_format: str = "auto"            # auto | dummy (random init) | safetensors
+
+    def replace(self, **kw) -> "EngineConfig":
+        return replace(self, **kw)
+
+    def as_dict(self) -> dict:
+        return asdict(self)
+
+    @staticmethod
+    def from_env(**overrides) -> "EngineConfig":
+        """Engine knobs from the reference's env variables (infra/docker-compose.yml:16-27)."""
+        cfg = EngineConfig()
+        env = os.environ
+        kw = {}
+        if env.get("LLM_MODEL"):
+            kw["model"] = env["LLM_MODEL"]
+        if env.get("LLM_DTYPE"):
+            kw["dtype"] = env["LLM_DTYPE"]
+        n = _env_int("LLM_MAX_NUM_SEQS", -1)
+        if n > 0:
+            kw["max_num_seqs"] = n
+        n = _env_int("LLM_MAX_NUM_BATCHED_TOKENS", -1)
+        if n > 0:
+            kw["max_num_batched_tokens"] = n
+        if env.get("LLM_GPU_MEMORY_UTILIZATION"):
+            kw["gpu_memory_utilization"] = float(env["LLM_GPU_MEMORY_UTILIZATION"])
+        n = _env_int("LLM_MAX_MODEL_LEN", 0)
+        if n > 0:
+            kw["max_model_len"] = n
+        n = _env_int("VLLM_BLOCK_SIZE", 0)
+        if n > 0:
+            kw["block_size"] = n
+        n = _env_int("LLM_TENSOR_PARALLEL_SIZE", 0)
+        if n > 0:
+            kw["tensor_parallel_size"] = n
+        kw.update({k: v for k, v in overrides.items() if v is not None})
+        return cfg.replace(**kw)

@@ -1,0 +1,192 @@
+"""Synchronous serving engine: scheduler + model runner + stop handling.
+
+The reference drives vLLM's ``AsyncLLMEngine.generate`` (llm/serve_llm.py:504-612); this
+engine provides the same contract (prompt in, streamed outputs, TTFT = time to the first
+yielded output) on the MI355X-native runner.  ``async_engine.AsyncEngine`` wraps it with
+a background step loop for the HTTP front end.
+"""
+from __future__ import annotations
+
+import random
+import threading
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from ..config import EngineConfig, resolve_model
+from .model_runner import ModelRunner
+from .scheduler import Scheduler
+from .sequence import SamplingParams, Sequence
+from .tokenizer import get_tokenizer
+
+
+@dataclass
+class RequestOutput:
+    request_id: str
+    token_ids: list
+    finished: bool
+    finish_reason: str | None = None
+    prompt_tokens: int = 0
+    cached_prompt_tokens: int = 0
+    arrival_time: float = 0.0
+    first_token_time: float | None = None
+    first_scheduled_time: float | None = None
+    finish_time: float | None = None
+    new_token_ids: list = field(default_factory=list)
+
+    @property
+    def completion_tokens(self) -> int:
+        return len(self.token_ids)
+
+    @property
+    def ttft(self) -> float | None:
+        if self.first_token_time is None:
+            return None
+        return self.first_token_time - self.arrival_time
+
+    @property
+    def queue_wait(self) -> float | None:
+        if self.first_scheduled_time is None:
+            return None
+        return self.first_scheduled_time - self.arrival_time
+
+
+@dataclass
+class StepStats:
+    num_seqs: int
+    num_tokens: int
+    num_decode: int
+    seconds: float
+
+
+class LLMEngine:
+    def __init__(self, cfg: EngineConfig, runner: ModelRunner | None = None, device=None):
+        self.cfg = cfg
+        self.model_cfg, weights_dir = resolve_model(cfg.model)
+        self.tokenizer = get_tokenizer(weights_dir or cfg.model, self.model_cfg.vocab_size)
+        dev = device or cfg.device
+        self.runner = runner or ModelRunner(cfg, self.model_cfg, dev, weights_dir=weights_dir)
+        self.scheduler = Scheduler(self.runner.bm, cfg.max_num_seqs, cfg.max_num_batched_tokens,
+                                   cfg.max_model_len, cfg.long_prefill_token_threshold)
+        self.eos_ids = set(self.model_cfg.eos_token_ids) | {self.tokenizer.eos_token_id}
+        self.lock = threading.RLock()
+        self.last_step: StepStats | None = None
+        self.total_steps = 0
+        self.total_generated = 0
+        self.total_prompt = 0
+        self.batch_size_history: list = []
+        self._rng = random.Random(cfg.seed)
+
+    # ------------------------------------------------------------------------------------
+    def add_request(self, request_id: str, prompt_ids, sampling: SamplingParams,
+                    arrival_time: float | None = None) -> Sequence:
+        ids = list(map(int, prompt_ids))
+        if not ids:
+            ids = [self.tokenizer.bos_token_id]
+        limit = self.cfg.max_model_len - 1
+        if len(ids) > limit:
+            ids = ids[:limit]
+        seq = Sequence(request_id=request_id, prompt_ids=ids, sampling=sampling)
+        if arrival_time is not None:
+            seq.arrival_time = arrival_time
+        seq.seed = sampling.seed if sampling.seed is not None else self._rng.getrandbits(62)
+        with self.lock:
+            self.scheduler.add(seq)
+        return seq
+
+    def abort(self, request_id: str):
+        with self.lock:
+            self.scheduler.abort(request_id)
+
+    def has_unfinished(self) -> bool:
+        return self.scheduler.has_work()
+
+    # ------------------------------------------------------------------------------------
+    def step(self) -> list[RequestOutput]:
+        with self.lock:
+            batch = self.scheduler.schedule()
+            if batch.empty:
+                return []
+            t0 = time.perf_counter()
+            toks = self.runner.execute(batch)
+            now = time.perf_counter()
+            outs = []
+            for seq, n, tok in zip(batch.seqs, batch.q_len, toks):
+                seq.num_computed += n
+                if seq.num_computed < seq.num_tokens:
+                    self.runner.bm.commit(seq.seq_id, seq.token_array(), seq.num_computed)
+                    continue  # chunked prefill not finished: sampled token discarded
+                tok = int(tok)
+                seq.append(tok)
+                if seq.first_token_time is None:
+                    seq.first_token_time = now
+                self.runner.bm.commit(seq.seq_id, seq.token_array(), seq.num_computed)
+                reason = self._stop_reason(seq, tok)
+                if reason:
+                    self.scheduler.finish(seq, reason)
+                outs.append(self._output(seq, [tok]))
+            self.total_steps += 1
+            self.total_generated += len(outs)
+            self.last_step = StepStats(len(batch.seqs), batch.num_tokens, batch.num_decode,
+                                       now - t0)
+            self.batch_size_history.append(len(batch.seqs))
+            if len(self.batch_size_history) > 4096:
+                del self.batch_size_history[:2048]
+            return outs
+
+    def _stop_reason(self, seq: Sequence, tok: int) -> str | None:
+        sp = seq.sampling
+        if not sp.ignore_eos and (tok in self.eos_ids or tok in sp.stop_token_ids):
+            return "stop"
+        if len(seq.output_ids) >= sp.max_tokens:
+            return "length"
+        if seq.num_tokens >= self.cfg.max_model_len:
+            return "length"
+        return None
+
+    def _output(self, seq: Sequence, new) -> RequestOutput:
+        return RequestOutput(
+            request_id=seq.request_id, token_ids=list(seq.output_ids), finished=seq.finished,
+            finish_reason=seq.finish_reason, prompt_tokens=seq.num_prompt,
+            cached_prompt_tokens=seq.num_cached_prompt, arrival_time=seq.arrival_time,
+            first_token_time=seq.first_token_time, first_scheduled_time=seq.first_scheduled_time,
+            finish_time=seq.finish_time, new_token_ids=list(new))
+
+    # ------------------------------------------------------------------------------------
+    def generate(self, prompts, sampling: SamplingParams | list) -> list[RequestOutput]:
+        """Blocking batch generation (prompts: list of token-id lists or strings)."""
+        if not isinstance(sampling, list):
+            sampling = [sampling] * len(prompts)
+        ids = []
+        for i, p in enumerate(prompts):
+            toks = self.tokenizer.encode(p) if isinstance(p, str) else p
+            rid = f"gen-{time.monotonic_ns()}-{i}"
+            self.add_request(rid, toks, sampling[i])
+            ids.append(rid)
+        final: dict[str, RequestOutput] = {}
+        while self.has_unfinished():
+            for o in self.step():
+                if o.finished:
+                    final[o.request_id] = o
+        return [final[r] for r in ids if r in final]
+
+    # ------------------------------------------------------------------------------------
+    def kv_cache_info(self) -> dict:
+        r = self.runner
+        return {
+            "num_gpu_blocks": r.num_blocks,
+            "block_size": r.block_size,
+            "total_tokens": r.kv_total_tokens,
+            "free_blocks": r.bm.num_free_blocks(),
+            "cached_blocks": r.bm.num_cached_blocks(),
+            "prefix_queries": r.bm.prefix_queries(),
+            "prefix_hits": r.bm.prefix_hits(),
+        }
+
+    def est_max_concurrency(self) -> float:
+        return self.runner.kv_total_tokens / max(1, self.cfg.max_model_len)
+
+
+def token_array(ids) -> np.ndarray:
+    return np.asarray(ids, dtype=np.int64)

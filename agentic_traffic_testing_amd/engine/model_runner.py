@@ -1,0 +1,320 @@
+"""Model runner: KV-cache allocation, per-step input preparation, hipGraph decode replay.
+
+One step = one forward over a decode-first ``Batch`` (scheduler.py) followed by sampling.
+
+* **KV cache** - one [L, nb, Hkv, BS, D] K tensor and one [L, nb, Hkv, D, BS] V tensor (V
+  transposed for the PV MFMA, see ops/csrc/attention.hip).  ``num_blocks`` comes from
+  ``gpu_memory_utilization`` of the device's HBM after weights and an activation reserve,
+  i.e. ~1.9 M tokens for Llama-3-8B at 0.9 of 288 GB.
+* **Metadata** - the native block manager emits int32 arrays which are packed into ONE
+  pinned host buffer and moved with ONE async H2D copy per step; every device metadata
+  tensor is a view into the matching device buffer.
+* **hipGraphs** - decode-only steps are padded to a bucket (1, 2, 4, 8, ...) and replayed
+  from a captured graph that contains the whole forward, the LM head and the sampler, so a
+  decode step costs one graph launch instead of ~330 kernel launches.
+"""
+from __future__ import annotations
+
+import math
+import time
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..config import EngineConfig, ModelConfig
+from ..models.llama import AttnMeta, LlamaModel, torch_dtype
+from ..ops import reference as ref
+from ..runtime import BlockManager
+from .scheduler import Batch
+
+
+def _even(n: int) -> int:
+    return n + (n & 1)
+
+
+class MetaLayout:
+    """int32-word layout of the packed per-step metadata buffer."""
+
+    def __init__(self, T: int, S: int, W: int, NT: int):
+        self.T, self.S, self.W, self.NT = T, S, W, NT
+        o = 0
+        self.fields = {}
+
+        def add(name, n, dtype=torch.int32):
+            nonlocal o
+            words = n * (2 if dtype == torch.int64 else 1)
+            if dtype == torch.int64:
+                o = _even(o)
+            self.fields[name] = (o, n, dtype)
+            o += words
+
+        add("input_ids", T)
+        add("positions", T)
+        add("slot_mapping", T)
+        add("block_tables", S * W)
+        add("seq_kvlen", S)
+        add("seq_qstart", S + 1)
+        add("tile_seq", NT)
+        add("tile_qoff", NT)
+        add("temperature", S, torch.float32)
+        add("logits_idx", S, torch.int64)
+        add("seeds", S, torch.int64)
+        add("steps", S, torch.int64)
+        self.size = _even(o)
+
+    def views(self, buf: torch.Tensor) -> dict:
+        out = {}
+        for name, (o, n, dt) in self.fields.items():
+            if dt == torch.int64:
+                out[name] = buf[o:o + 2 * n].view(torch.int64)
+            elif dt == torch.float32:
+                out[name] = buf[o:o + n].view(torch.float32)
+            else:
+                out[name] = buf[o:o + n]
+        out["block_tables"] = out["block_tables"].view(self.S, self.W)
+        return out
+
+    def pack(self, host: np.ndarray, arrays: dict):
+        for name, (o, n, dt) in self.fields.items():
+            a = arrays.get(name)
+            if a is None:
+                continue
+            if dt == torch.int64:
+                host[o:o + 2 * n].view(np.int64)[:len(a)] = a
+            elif dt == torch.float32:
+                host[o:o + n].view(np.float32)[:len(a)] = a
+            else:
+                host[o:o + n][:a.size] = a.reshape(-1)
+
+
+class ModelRunner:
+    def __init__(self, cfg: EngineConfig, model_cfg: ModelConfig, device: str = "cuda",
+                 tp_rank: int = 0, tp_size: int = 1, tp_group=None, weights_dir=None):
+        self.cfg = cfg
+        self.mcfg = model_cfg
+        self.device = torch.device(device)
+        self.is_cuda = self.device.type == "cuda"
+        self.dtype = torch_dtype(cfg.dtype)
+        self.tp_rank, self.tp_size = tp_rank, tp_size
+        t0 = time.perf_counter()
+        self.model = LlamaModel(model_cfg, self.dtype, self.device, tp_rank, tp_size, tp_group)
+        if weights_dir and cfg.load_format != "dummy":
+            self.model.load_safetensors(weights_dir)
+        else:
+            self.model.init_random(seed=cfg.seed)
+        self.load_seconds = time.perf_counter() - t0
+        self.block_size = cfg.block_size
+        self.bt_width = math.ceil(cfg.max_model_len / cfg.block_size)
+        self.part_tokens = cfg.decode_partition_tokens
+        self.max_parts = max(1, math.ceil(cfg.max_model_len / self.part_tokens))
+        self.tile_tokens = ops.PREFILL_TILE_TOKENS.get(self.model.g, 16)
+        self.graph_sizes = sorted(b for b in cfg.graph_batch_sizes)
+        cap = next((b for b in self.graph_sizes if b >= cfg.max_num_seqs), cfg.max_num_seqs)
+        self.graph_sizes = [b for b in self.graph_sizes if b <= cap]
+        self.max_seqs = max(cfg.max_num_seqs, self.graph_sizes[-1] if self.graph_sizes else 1)
+        self.max_tokens = cfg.max_num_batched_tokens + self.max_seqs
+        self._alloc_kv()
+        self.bm = BlockManager(self.num_blocks, self.block_size, cfg.enable_prefix_caching)
+        # metadata buffers (max layout)
+        self.max_layout = MetaLayout(self.max_tokens, self.max_seqs, self.bt_width,
+                                     self.max_tokens)
+        pin = self.is_cuda
+        self.meta_host = torch.zeros(self.max_layout.size, dtype=torch.int32, pin_memory=pin)
+        self.meta_host_np = self.meta_host.numpy()
+        self.meta_dev = torch.zeros(self.max_layout.size, dtype=torch.int32, device=self.device)
+        nkv = self.model.n_kv_heads
+        self.part_out = torch.empty(self.max_seqs * nkv * self.max_parts * 16 * 128,
+                                    dtype=torch.float32, device=self.device)
+        self.part_lse = torch.empty(self.max_seqs * nkv * self.max_parts * 16,
+                                    dtype=torch.float32, device=self.device)
+        self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        self.graph_io: dict[int, dict] = {}
+        self.graph_pool = None
+        self.steps = 0
+        self.graph_steps = 0
+
+    # ------------------------------------------------------------------------------------
+    def _alloc_kv(self):
+        m = self.model
+        L = self.mcfg.num_layers
+        per_block = 2 * L * m.n_kv_heads * self.block_size * m.head_dim * self.dtype.itemsize
+        if self.cfg.num_kv_blocks > 0:
+            nb = self.cfg.num_kv_blocks
+        elif self.is_cuda:
+            torch.cuda.synchronize()
+            free, total = torch.cuda.mem_get_info(self.device)
+            used = total - free
+            # activation / workspace reserve: logits + GEMM intermediates at the token budget
+            T = self.cfg.max_num_batched_tokens
+            act = T * (self.mcfg.hidden_size * 8 + (m.inter * 2 + m.qkv_width) * 2) * 2
+            act += self.max_seqs_estimate() * self.mcfg.vocab_size * 4 * 2 + (2 << 30)
+            budget = total * self.cfg.gpu_memory_utilization - used - act
+            nb = int(budget // per_block)
+        else:
+            nb = 256
+        nb = max(nb, 2 * self.bt_width)
+        self.num_blocks = nb
+        shape_k = (L, nb, m.n_kv_heads, self.block_size, m.head_dim)
+        shape_v = (L, nb, m.n_kv_heads, m.head_dim, self.block_size)
+        # zero-init: pages read past a sequence's end must hold finite values
+        self.k_cache = torch.zeros(shape_k, dtype=self.dtype, device=self.device)
+        self.v_cache = torch.zeros(shape_v, dtype=self.dtype, device=self.device)
+        self.k_layers = [self.k_cache[i] for i in range(L)]
+        self.v_layers = [self.v_cache[i] for i in range(L)]
+        self.kv_bytes = per_block * nb
+
+    def max_seqs_estimate(self) -> int:
+        return max(self.cfg.max_num_seqs, 16)
+
+    @property
+    def kv_total_tokens(self) -> int:
+        return self.num_blocks * self.block_size
+
+    # ------------------------------------------------------------------------------------
+    def _prepare(self, batch: Batch, pad_seqs: int = 0, tiles: bool = True):
+        ids, qs, ql = batch.arrays()
+        d = self.bm.build_batch(ids, qs, ql, self.bt_width,
+                                self.tile_tokens if tiles else 0, batch.num_decode, 0, pad_seqs)
+        T = d["positions"].shape[0]
+        S = d["seq_kvlen"].shape[0]
+        NT = d["tile_seq"].shape[0]
+        lay = MetaLayout(T, S, self.bt_width, NT)
+        input_ids = np.zeros(T, dtype=np.int32)
+        row = 0
+        temps = np.zeros(S, dtype=np.float32)
+        seeds = np.zeros(S, dtype=np.int64)
+        steps = np.zeros(S, dtype=np.int64)
+        for i, (seq, s0, n) in enumerate(zip(batch.seqs, batch.q_start, batch.q_len)):
+            input_ids[row:row + n] = seq.token_array()[s0:s0 + n]
+            row += n
+            temps[i] = seq.sampling.temperature
+            seeds[i] = seq.seed
+            steps[i] = len(seq.output_ids)
+        arrays = dict(d)
+        arrays.update(input_ids=input_ids, temperature=temps, seeds=seeds, steps=steps)
+        return lay, arrays
+
+    def _upload(self, lay: MetaLayout, arrays: dict, dev_buf=None):
+        host = self.meta_host_np[:lay.size]
+        lay.pack(host, arrays)
+        dev = self.meta_dev[:lay.size] if dev_buf is None else dev_buf
+        dev.copy_(self.meta_host[:lay.size], non_blocking=True)
+        return lay.views(dev)
+
+    def _meta(self, v: dict, num_decode: int, num_tiles: int) -> AttnMeta:
+        return AttnMeta(positions=v["positions"], slot_mapping=v["slot_mapping"],
+                        block_tables=v["block_tables"], seq_kvlen=v["seq_kvlen"],
+                        seq_qstart=v["seq_qstart"], tile_seq=v["tile_seq"],
+                        tile_qoff=v["tile_qoff"], logits_idx=v["logits_idx"],
+                        num_decode=num_decode, num_tiles=num_tiles)
+
+    def _forward_sample(self, v: dict, md: AttnMeta, num_parts: int, special_sampling=None):
+        m = self.model
+        hidden = m.forward(v["input_ids"], md, self.k_layers, self.v_layers, self.part_out,
+                           self.part_lse, num_parts, self.part_tokens)
+        last = hidden.index_select(0, v["logits_idx"])
+        logits = m.compute_logits(last)
+        if special_sampling is not None:
+            return special_sampling(logits)
+        return ops.sample(logits, v["temperature"], v["seeds"], v["steps"])
+
+    # ------------------------------------------------------------------------------------
+    def execute(self, batch: Batch) -> np.ndarray:
+        """Run one step; returns sampled token ids (one per sequence in batch order)."""
+        n = len(batch.seqs)
+        self.steps += 1
+        special = any(s.sampling.top_p < 1.0 or s.sampling.top_k > 0 for s in batch.seqs)
+        decode_only = batch.num_decode == n
+        if (self.is_cuda and self.cfg.use_graphs and decode_only and not special
+                and self.graph_sizes and n <= self.graph_sizes[-1]):
+            bucket = next(b for b in self.graph_sizes if b >= n)
+            if bucket not in self.graphs:
+                self.capture(bucket)
+            io = self.graph_io[bucket]
+            lay, arrays = self._prepare(batch, pad_seqs=bucket, tiles=False)
+            assert lay.size == io["layout"].size
+            self._upload(lay, arrays, io["dev"])
+            self.graphs[bucket].replay()
+            self.graph_steps += 1
+            return io["out"][:n].cpu().numpy()
+        lay, arrays = self._prepare(batch)
+        v = self._upload(lay, arrays)
+        md = self._meta(v, batch.num_decode, lay.NT)
+        max_kv = int(arrays["seq_kvlen"][:batch.num_decode].max()) if batch.num_decode else 0
+        num_parts = max(1, math.ceil(max_kv / self.part_tokens))
+        sampler = None
+        if special:
+            sampler = self._special_sampler(batch)
+        toks = self._forward_sample(v, md, num_parts, sampler)
+        return toks.cpu().numpy()
+
+    def _special_sampler(self, batch: Batch):
+        params = [s.sampling for s in batch.seqs]
+        seqs = list(batch.seqs)
+
+        def fn(logits):
+            out = torch.empty(logits.shape[0], dtype=torch.long, device=logits.device)
+            for i, (p, seq) in enumerate(zip(params, seqs)):
+                row = logits[i].float()
+                if not p.temperature > 1e-5:
+                    out[i] = torch.argmax(row)
+                    continue
+                row = row / p.temperature
+                if p.top_k > 0:
+                    kth = torch.topk(row, min(p.top_k, row.numel())).values[-1]
+                    row = row.masked_fill(row < kth, float("-inf"))
+                probs = torch.softmax(row, -1)
+                if p.top_p < 1.0:
+                    sp, si = torch.sort(probs, descending=True)
+                    cum = torch.cumsum(sp, 0)
+                    keep = cum - sp < p.top_p
+                    mask = torch.zeros_like(probs, dtype=torch.bool)
+                    mask[si[keep]] = True
+                    probs = torch.where(mask, probs, torch.zeros_like(probs))
+                    probs = probs / probs.sum()
+                g = torch.Generator(device=logits.device)
+                g.manual_seed((seq.seed * 1000003 + len(seq.output_ids)) & 0x7FFFFFFFFFFFFFFF)
+                out[i] = torch.multinomial(probs, 1, generator=g)[0]
+            return out
+        return fn
+
+    # ------------------------------------------------------------------------------------
+    def capture(self, bucket: int):
+        """Capture a decode step for `bucket` sequences into a hipGraph."""
+        lay = MetaLayout(bucket, bucket, self.bt_width, 0)
+        dev = torch.zeros(lay.size, dtype=torch.int32, device=self.device)
+        v = lay.views(dev)
+        # dummy sequences: kvlen 0, slot -1 -> kernels skip them
+        v["seq_qstart"].copy_(torch.arange(bucket + 1, dtype=torch.int32))
+        v["slot_mapping"].fill_(-1)
+        v["logits_idx"].copy_(torch.arange(bucket, dtype=torch.int64))
+        md = self._meta(v, bucket, 0)
+        stream = torch.cuda.Stream(self.device)
+        stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(stream):
+            for _ in range(2):  # warm up (hipBLASLt heuristics, allocator)
+                self._forward_sample(v, md, self.max_parts)
+        torch.cuda.current_stream(self.device).wait_stream(stream)
+        g = torch.cuda.CUDAGraph()
+        if self.graph_pool is None:
+            self.graph_pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
+            out = self._forward_sample(v, md, self.max_parts)
+        torch.cuda.synchronize(self.device)
+        self.graphs[bucket] = g
+        self.graph_io[bucket] = {"layout": lay, "dev": dev, "out": out}
+
+    def capture_all(self):
+        if not (self.is_cuda and self.cfg.use_graphs):
+            return
+        for b in self.graph_sizes:
+            if b not in self.graphs:
+                self.capture(b)
+
+    def reset_state(self):
+        """Drop prefix cache contents (used between benchmark phases)."""
+        self.bm.reset_prefix_cache()
+
+
+__all__ = ["ModelRunner", "MetaLayout", "ref"]

@@ -1,0 +1,250 @@
+"""Llama-3 decoder (8B / 70B / 3.2 shapes) over the atta op layer.
+
+This is the model vLLM executes inside ``AsyncLLMEngine`` for the reference
+(llm/serve_llm.py:362-378; model id from infra/docker-compose.yml:26).  MI355X design:
+
+* weights are stored pre-fused: ``qkv`` [(Hq+2Hkv)*D, H], ``gate_up`` [2I, H] so each layer
+  runs 4 GEMMs (hipBLASLt via F.linear for prefill-sized M; the decode path can swap in
+  the fused GEMV kernels of ``ops``), and every elementwise step is a hand-written kernel:
+  fused residual-add+RMSNorm, RoPE+paged-KV write, paged attention (prefill and decode
+  variants), SiLU-mul, sampler;
+* tensor parallelism is Megatron-style: qkv / gate_up column-parallel, o / down row-parallel
+  with one all-reduce each (``parallel.comm``); the embedding is replicated and the LM head
+  is vocab-parallel with an all-gather of the [B, V/tp] logits;
+* weights are either seeded random-init (benchmarks: no network, gated checkpoints) or
+  loaded from HF safetensors.
+"""
+from __future__ import annotations
+
+import json
+import math
+from dataclasses import dataclass
+from pathlib import Path
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..config import ModelConfig
+from ..ops import reference as ref
+
+DTYPES = {"bfloat16": torch.bfloat16, "bf16": torch.bfloat16, "float16": torch.float16,
+          "fp16": torch.float16, "half": torch.float16, "auto": torch.bfloat16}
+
+
+def torch_dtype(name: str) -> torch.dtype:
+    return DTYPES.get(str(name).replace("torch.", ""), torch.bfloat16)
+
+
+@dataclass
+class AttnMeta:
+    """Per-step attention metadata (all device tensors, built by the model runner)."""
+    positions: torch.Tensor       # int32 [T]
+    slot_mapping: torch.Tensor    # int32 [T]
+    block_tables: torch.Tensor    # int32 [S, W]
+    seq_kvlen: torch.Tensor       # int32 [S]
+    seq_qstart: torch.Tensor      # int32 [S+1]
+    tile_seq: torch.Tensor        # int32 [tiles]   (prefill sequences)
+    tile_qoff: torch.Tensor       # int32 [tiles]
+    logits_idx: torch.Tensor      # int64 [S]
+    num_decode: int               # sequences [0, num_decode) have exactly one query token
+    num_tiles: int
+
+
+@dataclass
+class LayerWeights:
+    input_norm: torch.Tensor
+    qkv: torch.Tensor
+    o: torch.Tensor
+    post_norm: torch.Tensor
+    gate_up: torch.Tensor
+    down: torch.Tensor
+
+
+class LlamaModel:
+    def __init__(self, cfg: ModelConfig, dtype=torch.bfloat16, device="cuda", tp_rank: int = 0,
+                 tp_size: int = 1, tp_group=None):
+        self.cfg = cfg
+        self.dtype = dtype
+        self.device = torch.device(device)
+        self.tp_rank, self.tp_size, self.tp_group = tp_rank, tp_size, tp_group
+        if cfg.num_heads % tp_size:
+            raise ValueError(f"num_heads {cfg.num_heads} not divisible by tp {tp_size}")
+        self.n_heads = cfg.num_heads // tp_size
+        # KV heads are split when possible, replicated when tp > num_kv_heads
+        self.kv_rep = max(1, tp_size // cfg.num_kv_heads)
+        self.n_kv_heads = max(1, cfg.num_kv_heads // tp_size)
+        self.head_dim = cfg.head_dim
+        self.inter = cfg.intermediate_size // tp_size
+        if cfg.intermediate_size % tp_size or cfg.vocab_size % tp_size:
+            raise ValueError("intermediate/vocab not divisible by tp")
+        self.vocab_shard = cfg.vocab_size // tp_size
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self.layers: list[LayerWeights] = []
+        self.embed = None
+        self.norm = None
+        self.lm_head = None
+        self.cos_sin = ref.rope_cos_sin(cfg.head_dim, min(cfg.max_position_embeddings, 1 << 17),
+                                        cfg.rope_theta, cfg.rope_scaling, device=self.device)
+        self.g = self.n_heads // self.n_kv_heads
+        if self.head_dim != 128 and self.device.type == "cuda":
+            raise ValueError("HIP attention kernels require head_dim 128")
+
+    # ---------------------------------------------------------------------------------
+    @property
+    def qkv_width(self) -> int:
+        return (self.n_heads + 2 * self.n_kv_heads) * self.head_dim
+
+    def init_random(self, seed: int = 0, std: float = 0.02):
+        """Seeded random-init weights of the full architecture (each rank draws its shard
+        from the full-model generator stream so TP=N reproduces TP=1 exactly)."""
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        gen_dev = dev if dev.type == "cuda" else torch.device("cpu")
+        g = torch.Generator(device=gen_dev)
+
+        def rnd(shape, tag: int, scale=std):
+            g.manual_seed(seed * 1000003 + tag)
+            return (torch.randn(shape, generator=g, device=gen_dev, dtype=torch.float32)
+                    * scale).to(dt).to(dev)
+
+        H, D = cfg.hidden_size, cfg.head_dim
+        self.embed = rnd((cfg.vocab_size, H), 1, 1.0)
+        self.norm = torch.ones(H, dtype=dt, device=dev)
+        lm = self.embed if cfg.tie_word_embeddings else rnd((cfg.vocab_size, H), 2)
+        self.lm_head = self._shard_rows(lm, self.vocab_shard).contiguous()
+        self.layers = []
+        for i in range(cfg.num_layers):
+            base = 100 + i * 10
+            wq = rnd((cfg.q_size, H), base + 0)
+            wk = rnd((cfg.kv_size, H), base + 1)
+            wv = rnd((cfg.kv_size, H), base + 2)
+            wo = rnd((H, cfg.q_size), base + 3)
+            wg = rnd((cfg.intermediate_size, H), base + 4)
+            wu = rnd((cfg.intermediate_size, H), base + 5)
+            wd = rnd((H, cfg.intermediate_size), base + 6) / math.sqrt(2 * cfg.num_layers) * 4
+            self.layers.append(self._make_layer(wq, wk, wv, wo, wg, wu, wd,
+                                                torch.ones(H, dtype=dt, device=dev),
+                                                torch.ones(H, dtype=dt, device=dev)))
+            del wq, wk, wv, wo, wg, wu, wd
+        return self
+
+    def _shard_rows(self, w: torch.Tensor, rows: int) -> torch.Tensor:
+        if self.tp_size == 1:
+            return w
+        return w[self.tp_rank * rows:(self.tp_rank + 1) * rows]
+
+    def _shard_cols(self, w: torch.Tensor, cols: int) -> torch.Tensor:
+        if self.tp_size == 1:
+            return w
+        return w[:, self.tp_rank * cols:(self.tp_rank + 1) * cols]
+
+    def _make_layer(self, wq, wk, wv, wo, wg, wu, wd, n_in, n_post) -> LayerWeights:
+        D = self.head_dim
+        q = self._shard_rows(wq, self.n_heads * D)
+        kv_rank = self.tp_rank // self.kv_rep
+        if self.tp_size == 1:
+            k, v = wk, wv
+        else:
+            k = wk[kv_rank * self.n_kv_heads * D:(kv_rank + 1) * self.n_kv_heads * D]
+            v = wv[kv_rank * self.n_kv_heads * D:(kv_rank + 1) * self.n_kv_heads * D]
+        qkv = torch.cat([q, k, v], 0).contiguous()
+        o = self._shard_cols(wo, self.n_heads * D).contiguous()
+        gu = torch.cat([self._shard_rows(wg, self.inter), self._shard_rows(wu, self.inter)],
+                       0).contiguous()
+        down = self._shard_cols(wd, self.inter).contiguous()
+        return LayerWeights(n_in.contiguous(), qkv, o, n_post.contiguous(), gu, down)
+
+    def load_safetensors(self, path: str):
+        """Load HF Llama weights (model*.safetensors) and shard for this TP rank."""
+        from safetensors import safe_open
+
+        p = Path(path)
+        files = sorted(p.glob("*.safetensors"))
+        if not files:
+            raise FileNotFoundError(f"no safetensors in {path}")
+        index = {}
+        for f in files:
+            with safe_open(str(f), framework="pt") as sf:
+                for k in sf.keys():
+                    index[k] = f
+
+        def get(name):
+            with safe_open(str(index[name]), framework="pt") as sf:
+                return sf.get_tensor(name).to(self.dtype).to(self.device)
+
+        cfg = self.cfg
+        self.embed = get("model.embed_tokens.weight")
+        self.norm = get("model.norm.weight")
+        lm = self.embed if cfg.tie_word_embeddings or "lm_head.weight" not in index else get(
+            "lm_head.weight")
+        self.lm_head = self._shard_rows(lm, self.vocab_shard).contiguous()
+        self.layers = []
+        for i in range(cfg.num_layers):
+            pre = f"model.layers.{i}."
+            self.layers.append(self._make_layer(
+                get(pre + "self_attn.q_proj.weight"), get(pre + "self_attn.k_proj.weight"),
+                get(pre + "self_attn.v_proj.weight"), get(pre + "self_attn.o_proj.weight"),
+                get(pre + "mlp.gate_proj.weight"), get(pre + "mlp.up_proj.weight"),
+                get(pre + "mlp.down_proj.weight"), get(pre + "input_layernorm.weight"),
+                get(pre + "post_attention_layernorm.weight")))
+        return self
+
+    # ---------------------------------------------------------------------------------
+    def weight_bytes(self) -> int:
+        n = self.embed.numel() + self.norm.numel() + self.lm_head.numel()
+        for l in self.layers:
+            n += sum(t.numel() for t in (l.input_norm, l.qkv, l.o, l.post_norm, l.gate_up, l.down))
+        return n * self.embed.element_size()
+
+    def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+        if self.tp_size > 1:
+            from ..parallel import comm
+
+            comm.tp_all_reduce(x, self.tp_group)
+        return x
+
+    def forward(self, input_ids: torch.Tensor, md: AttnMeta, k_caches, v_caches,
+                part_out=None, part_lse=None, num_parts: int = 1, part_tokens: int = 256):
+        """Returns the final normed hidden state rows [T, H]."""
+        cfg = self.cfg
+        eps = cfg.rms_norm_eps
+        h = F.embedding(input_ids, self.embed)
+        T = h.shape[0]
+        residual = torch.empty_like(h)
+        nq, nkv, D = self.n_heads, self.n_kv_heads, self.head_dim
+        for li, L in enumerate(self.layers):
+            if li == 0:
+                residual.copy_(h)
+                x = ops.rms_norm(h, L.input_norm, eps)
+            else:
+                x = ops.fused_add_rms_norm(h, residual, L.input_norm, eps)
+            qkv = F.linear(x, L.qkv)
+            q = ops.rope_cache(qkv, md.positions, md.slot_mapping, self.cos_sin, k_caches[li],
+                               v_caches[li], nq, nkv, D)
+            attn = torch.empty_like(q)
+            if md.num_decode > 0:
+                ops.attention_decode(q, k_caches[li], v_caches[li], md.block_tables,
+                                     md.seq_kvlen, md.seq_qstart, self.scale, part_out, part_lse,
+                                     num_parts, part_tokens, out=attn, num_seqs=md.num_decode)
+            if md.num_tiles > 0:
+                ops.attention_prefill(q, k_caches[li], v_caches[li], md.block_tables,
+                                      md.seq_kvlen, md.seq_qstart, md.tile_seq, md.tile_qoff,
+                                      self.scale, out=attn)
+            h = self._all_reduce(F.linear(attn.view(T, nq * D), L.o))
+            x = ops.fused_add_rms_norm(h, residual, L.post_norm, eps)
+            gu = F.linear(x, L.gate_up)
+            a = ops.silu_and_mul(gu)
+            h = self._all_reduce(F.linear(a, L.down))
+        return ops.fused_add_rms_norm(h, residual, self.norm, eps)
+
+    def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        logits = F.linear(hidden, self.lm_head)
+        if self.tp_size > 1:
+            from ..parallel import comm
+
+            logits = comm.tp_all_gather_last(logits, self.tp_group)
+        return logits
+
+
+def save_config_json(cfg: ModelConfig, path: str):
+    Path(path).write_text(json.dumps(cfg.__dict__, indent=2, default=list))

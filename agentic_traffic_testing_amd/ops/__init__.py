@@ -1,0 +1,153 @@
+"""Op layer: CDNA4 HIP kernels (``torch.ops.atta``) with device-strict dispatch.
+
+* GPU tensors always run the hand-written HIP kernels from ``_atta_kernels.so``.  If the
+  library is missing or fails to load, GPU calls raise ``NativeKernelsUnavailable`` -
+  there is no silent eager fallback on a GPU.
+* CPU tensors run ``reference.py`` (the same math in fp32 PyTorch) so the whole engine can
+  be exercised in the CPU test tier.
+"""
+from __future__ import annotations
+
+import os
+from pathlib import Path
+
+import torch
+
+from . import reference as ref
+
+_LIB = Path(__file__).resolve().parent / "_atta_kernels.so"
+_loaded = False
+_load_error: str | None = None
+
+
+class NativeKernelsUnavailable(RuntimeError):
+    pass
+
+
+def load_native(build_if_missing: bool = True) -> bool:
+    """Load the HIP kernel library (building it in-tree first if needed)."""
+    global _loaded, _load_error
+    if _loaded:
+        return True
+    try:
+        if not _LIB.exists() and build_if_missing:
+            from .build import build_kernels
+
+            build_kernels()
+        torch.ops.load_library(str(_LIB))
+        _loaded = True
+        _load_error = None
+    except Exception as e:  # pragma: no cover - depends on environment
+        _load_error = f"{type(e).__name__}: {e}"
+    return _loaded
+
+
+def native_available() -> bool:
+    return load_native(build_if_missing=os.environ.get("ATTA_NO_BUILD", "0") != "1")
+
+
+def _native():
+    if not native_available():
+        raise NativeKernelsUnavailable(
+            f"atta HIP kernels not loadable from {_LIB}: {_load_error}. "
+            "Run `python -m agentic_traffic_testing_amd.ops.build`.")
+    return torch.ops.atta
+
+
+# ---------------------------------------------------------------------------------------
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor | None = None):
+    if not x.is_cuda:
+        r = ref.rms_norm(x, w, eps)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    out = torch.empty_like(x) if out is None else out
+    _native().rms_norm(out, x, w, eps)
+    return out
+
+
+def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                       out: torch.Tensor | None = None):
+    """residual <- x + residual (in place); returns rmsnorm(residual) * w."""
+    if not x.is_cuda:
+        n, r = ref.fused_add_rms_norm(x, residual, w, eps)
+        residual.copy_(r)
+        if out is not None:
+            out.copy_(n)
+            return out
+        return n
+    out = torch.empty_like(x) if out is None else out
+    _native().fused_add_rms_norm(out, residual, x, w, eps)
+    return out
+
+
+def silu_and_mul(x: torch.Tensor, out: torch.Tensor | None = None):
+    if not x.is_cuda:
+        r = ref.silu_and_mul(x)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    if out is None:
+        out = torch.empty(x.shape[0], x.shape[1] // 2, dtype=x.dtype, device=x.device)
+    _native().silu_and_mul(out, x)
+    return out
+
+
+def rope_cache(qkv, positions, slot_mapping, cos_sin, k_cache, v_cache, n_q_heads, n_kv_heads,
+               head_dim, q_out: torch.Tensor | None = None):
+    """Rotate q/k, write k/v to the paged cache; returns q [T, Hq, D]."""
+    if not qkv.is_cuda:
+        q = ref.rope_cache(qkv, positions, slot_mapping, cos_sin, k_cache, v_cache, n_q_heads,
+                           n_kv_heads, head_dim)
+        if q_out is not None:
+            q_out.copy_(q)
+            return q_out
+        return q
+    if q_out is None:
+        q_out = torch.empty(qkv.shape[0], n_q_heads, head_dim, dtype=qkv.dtype, device=qkv.device)
+    _native().rope_cache(q_out, k_cache, v_cache, qkv, positions, slot_mapping, cos_sin,
+                         n_q_heads, n_kv_heads, head_dim)
+    return q_out
+
+
+def attention_prefill(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, tile_seq,
+                      tile_qoff, scale, out=None):
+    if not q.is_cuda:
+        return ref.paged_attention(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart,
+                                   scale, out=out)
+    out = torch.empty_like(q) if out is None else out
+    _native().attention_prefill(out, q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart,
+                                tile_seq, tile_qoff, q.shape[1], k_cache.shape[1], scale)
+    return out
+
+
+def attention_decode(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, scale,
+                     part_out, part_lse, num_parts, part_tokens, out=None, num_seqs: int = -1):
+    """Decode attention for sequences [0, num_seqs) (one query token each)."""
+    if not q.is_cuda:
+        n = seq_kvlen.shape[0] if num_seqs < 0 else num_seqs
+        return ref.paged_attention(q, k_cache, v_cache, block_tables[:n], seq_kvlen[:n],
+                                   seq_qstart[:n + 1], scale, out=out)
+    out = torch.empty_like(q) if out is None else out
+    _native().attention_decode(out, part_out, part_lse, q, k_cache, v_cache, block_tables,
+                               seq_kvlen, seq_qstart, num_seqs, num_parts, part_tokens, q.shape[1],
+                               k_cache.shape[1], scale)
+    return out
+
+
+def sample(logits, temperature, seeds, steps, out=None):
+    if not logits.is_cuda:
+        r = ref.sample(logits, temperature, seeds, steps)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    if out is None:
+        out = torch.empty(logits.shape[0], dtype=torch.long, device=logits.device)
+    _native().sample(out, logits, temperature, seeds, steps)
+    return out
+
+
+PREFILL_TILE_TOKENS = {1: 64, 2: 32, 4: 16, 8: 8}  # tokens per prefill workgroup by GQA group

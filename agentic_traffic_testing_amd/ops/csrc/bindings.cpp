@@ -1,0 +1,185 @@
+// Torch operator registration for the CDNA4 kernel library (namespace `atta`).
+//
+// Each op validates shapes/dtypes on the host, then calls the raw-pointer launcher on
+// the current HIP stream, so ops are safe inside torch.cuda.graph capture (no
+// allocation, no sync).  Ops only accept device tensors: CPU execution of the same math
+// lives in ops/reference.py and is selected by the Python wrappers by tensor device,
+// never as a silent fallback for a GPU tensor.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "kernels.h"
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+int dtype_code(const at::Tensor& t) {
+  if (t.scalar_type() == at::kBFloat16) return 0;
+  if (t.scalar_type() == at::kHalf) return 1;
+  TORCH_CHECK(false, "atta: expected bf16/fp16 tensor, got ", t.scalar_type());
+}
+
+void check_rc(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, "atta::", what, " launch failed (rc=", rc, ")");
+}
+
+void check_dev(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "atta: ", name, " must be a GPU tensor");
+}
+
+void rms_norm(at::Tensor out, const at::Tensor& x, const at::Tensor& w, double eps) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && out.stride(1) == 1, "rms_norm: 2-D rows");
+  c10::hip::HIPGuard g(x.device());
+  check_rc(atta_rms_norm(out.data_ptr(), nullptr, x.data_ptr(), w.data_ptr(), x.size(0),
+                         x.size(1), x.stride(0), out.stride(0), 0, static_cast<float>(eps),
+                         dtype_code(x), cur_stream()),
+           "rms_norm");
+}
+
+void fused_add_rms_norm(at::Tensor out, at::Tensor residual, const at::Tensor& x,
+                        const at::Tensor& w, double eps) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && residual.stride(1) == 1 && out.stride(1) == 1,
+              "fused_add_rms_norm: 2-D rows");
+  TORCH_CHECK(residual.sizes() == x.sizes(), "fused_add_rms_norm: residual shape");
+  c10::hip::HIPGuard g(x.device());
+  check_rc(atta_rms_norm(out.data_ptr(), residual.data_ptr(), x.data_ptr(), w.data_ptr(),
+                         x.size(0), x.size(1), x.stride(0), out.stride(0), residual.stride(0),
+                         static_cast<float>(eps), dtype_code(x), cur_stream()),
+           "fused_add_rms_norm");
+}
+
+void silu_and_mul(at::Tensor out, const at::Tensor& x) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.size(1) % 2 == 0 && x.stride(1) == 1, "silu_and_mul: x");
+  TORCH_CHECK(out.size(1) * 2 == x.size(1) && out.size(0) == x.size(0), "silu_and_mul: out");
+  c10::hip::HIPGuard g(x.device());
+  check_rc(atta_silu_and_mul(out.data_ptr(), x.data_ptr(), x.size(0), out.size(1), x.stride(0),
+                             out.stride(0), dtype_code(x), cur_stream()),
+           "silu_and_mul");
+}
+
+void rope_cache(at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache, const at::Tensor& qkv,
+                const at::Tensor& positions, const at::Tensor& slot_mapping,
+                const at::Tensor& cos_sin, int64_t n_q_heads, int64_t n_kv_heads,
+                int64_t head_dim) {
+  check_dev(qkv, "qkv");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1, "rope_cache: qkv 2-D");
+  TORCH_CHECK(qkv.size(1) >= (n_q_heads + 2 * n_kv_heads) * head_dim, "rope_cache: qkv width");
+  TORCH_CHECK(positions.scalar_type() == at::kInt && slot_mapping.scalar_type() == at::kInt,
+              "rope_cache: positions/slot_mapping int32");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(1) == head_dim,
+              "rope_cache: cos_sin [max_pos, head_dim] fp32");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == n_kv_heads && k_cache.size(3) == head_dim,
+              "rope_cache: k_cache [nb, Hkv, BS, D]");
+  TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(2) == head_dim, "rope_cache: v_cache [nb,Hkv,D,BS]");
+  const int64_t q_out_stride = q_out.dim() == 3 ? q_out.stride(0) : q_out.stride(0);
+  c10::hip::HIPGuard g(qkv.device());
+  check_rc(atta_rope_cache(q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                           qkv.data_ptr(), positions.data_ptr<int>(),
+                           slot_mapping.data_ptr<int>(), cos_sin.data_ptr<float>(),
+                           qkv.size(0), n_q_heads, n_kv_heads, head_dim, k_cache.size(2),
+                           qkv.stride(0), q_out_stride, dtype_code(qkv), cur_stream()),
+           "rope_cache");
+}
+
+void attention_prefill(at::Tensor out, const at::Tensor& q, const at::Tensor& k_cache,
+                       const at::Tensor& v_cache, const at::Tensor& block_tables,
+                       const at::Tensor& seq_kvlen, const at::Tensor& seq_qstart,
+                       const at::Tensor& tile_seq, const at::Tensor& tile_qoff, int64_t n_q_heads,
+                       int64_t n_kv_heads, double scale) {
+  check_dev(q, "q");
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && seq_kvlen.scalar_type() == at::kInt &&
+                  seq_qstart.scalar_type() == at::kInt && tile_seq.scalar_type() == at::kInt &&
+                  tile_qoff.scalar_type() == at::kInt,
+              "attention_prefill: metadata must be int32");
+  TORCH_CHECK(q.stride(-1) == 1 && out.stride(-1) == 1, "attention_prefill: last dim contiguous");
+  c10::hip::HIPGuard g(q.device());
+  check_rc(atta_attention_prefill(
+               out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+               block_tables.data_ptr<int>(), seq_kvlen.data_ptr<int>(), seq_qstart.data_ptr<int>(),
+               tile_seq.data_ptr<int>(), tile_qoff.data_ptr<int>(), tile_seq.size(0), n_q_heads,
+               n_kv_heads, k_cache.size(3), k_cache.size(2), block_tables.stride(0), q.stride(0),
+               out.stride(0), static_cast<float>(scale), dtype_code(q), cur_stream()),
+           "attention_prefill");
+}
+
+void attention_decode(at::Tensor out, at::Tensor part_out, at::Tensor part_lse,
+                      const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                      const at::Tensor& block_tables, const at::Tensor& seq_kvlen,
+                      const at::Tensor& seq_qstart, int64_t num_seqs, int64_t num_parts,
+                      int64_t part_tokens, int64_t n_q_heads, int64_t n_kv_heads, double scale) {
+  check_dev(q, "q");
+  if (num_seqs < 0) num_seqs = seq_kvlen.size(0);
+  TORCH_CHECK(num_seqs <= seq_kvlen.size(0), "attention_decode: num_seqs");
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && seq_kvlen.scalar_type() == at::kInt &&
+                  seq_qstart.scalar_type() == at::kInt,
+              "attention_decode: metadata must be int32");
+  if (num_parts > 1) {
+    TORCH_CHECK(part_out.numel() >= num_seqs * n_kv_heads * num_parts * 16 * 128 &&
+                    part_lse.numel() >= num_seqs * n_kv_heads * num_parts * 16,
+                "attention_decode: partition workspace too small");
+  }
+  c10::hip::HIPGuard g(q.device());
+  check_rc(atta_attention_decode(
+               out.data_ptr(), part_out.data_ptr<float>(), part_lse.data_ptr<float>(),
+               q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
+               seq_kvlen.data_ptr<int>(), seq_qstart.data_ptr<int>(), num_seqs, num_parts,
+               part_tokens, n_q_heads, n_kv_heads, k_cache.size(3), k_cache.size(2),
+               block_tables.stride(0), q.stride(0), out.stride(0), static_cast<float>(scale),
+               dtype_code(q), cur_stream()),
+           "attention_decode");
+}
+
+void sample(at::Tensor out, const at::Tensor& logits, const at::Tensor& temperature,
+            const at::Tensor& seeds, const at::Tensor& steps) {
+  check_dev(logits, "logits");
+  TORCH_CHECK(out.scalar_type() == at::kLong && seeds.scalar_type() == at::kLong &&
+                  steps.scalar_type() == at::kLong && temperature.scalar_type() == at::kFloat,
+              "sample: dtypes");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "sample: logits 2-D");
+  const bool is_f32 = logits.scalar_type() == at::kFloat;
+  TORCH_CHECK(is_f32 || logits.scalar_type() == at::kBFloat16, "sample: logits fp32/bf16");
+  c10::hip::HIPGuard g(logits.device());
+  check_rc(atta_sample(out.data_ptr<int64_t>(), logits.data_ptr(), logits.size(0),
+                       logits.size(1), logits.stride(0), is_f32 ? 1 : 0,
+                       temperature.data_ptr<float>(), seeds.data_ptr<int64_t>(),
+                       steps.data_ptr<int64_t>(), cur_stream()),
+           "sample");
+}
+
+}  // namespace
+
+TORCH_LIBRARY(atta, m) {
+  m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
+  m.def("fused_add_rms_norm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");
+  m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
+  m.def(
+      "rope_cache(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor qkv, "
+      "Tensor positions, Tensor slot_mapping, Tensor cos_sin, int n_q_heads, int n_kv_heads, "
+      "int head_dim) -> ()");
+  m.def(
+      "attention_prefill(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
+      "Tensor block_tables, Tensor seq_kvlen, Tensor seq_qstart, Tensor tile_seq, "
+      "Tensor tile_qoff, int n_q_heads, int n_kv_heads, float scale) -> ()");
+  m.def(
+      "attention_decode(Tensor(a!) out, Tensor(b!) part_out, Tensor(c!) part_lse, Tensor q, "
+      "Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor seq_kvlen, "
+      "Tensor seq_qstart, int num_seqs, int num_parts, int part_tokens, int n_q_heads, int n_kv_heads, "
+      "float scale) -> ()");
+  m.def("sample(Tensor(a!) out, Tensor logits, Tensor temperature, Tensor seeds, Tensor steps) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(atta, CUDA, m) {
+  m.impl("rms_norm", &rms_norm);
+  m.impl("fused_add_rms_norm", &fused_add_rms_norm);
+  m.impl("silu_and_mul", &silu_and_mul);
+  m.impl("rope_cache", &rope_cache);
+  m.impl("attention_prefill", &attention_prefill);
+  m.impl("attention_decode", &attention_decode);
+  m.impl("sample", &sample);
+}

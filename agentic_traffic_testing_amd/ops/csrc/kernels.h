@@ -1,0 +1,37 @@
+// Host-side launcher declarations for the CDNA4 kernel library.  Every launcher takes raw
+// device pointers plus the HIP stream to launch on (graph-capture safe: no allocation, no
+// synchronisation) and returns 0 on success, -1 for an unsupported shape, or a hipError_t.
+// dtype: 0 = bf16, 1 = fp16.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+int atta_rms_norm(void* out, void* residual, const void* x, const void* w, int rows, int hidden,
+                  int64_t x_stride, int64_t out_stride, int64_t res_stride, float eps, int dtype,
+                  hipStream_t stream);
+
+int atta_silu_and_mul(void* out, const void* x, int rows, int inter, int64_t x_stride,
+                      int64_t out_stride, int dtype, hipStream_t stream);
+
+int atta_rope_cache(void* q_out, void* k_cache, void* v_cache, const void* qkv,
+                    const int* positions, const int* slot_mapping, const float* cos_sin,
+                    int num_tokens, int n_q_heads, int n_kv_heads, int head_dim, int block_size,
+                    int64_t qkv_stride, int64_t q_out_stride, int dtype, hipStream_t stream);
+
+int atta_attention_prefill(void* out, const void* q, const void* k_cache, const void* v_cache,
+                           const int* block_tables, const int* seq_kvlen, const int* seq_qstart,
+                           const int* tile_seq, const int* tile_qoff, int num_tiles,
+                           int n_q_heads, int n_kv_heads, int head_dim, int block_size,
+                           int bt_stride, int64_t q_stride, int64_t out_stride, float scale,
+                           int dtype, hipStream_t stream);
+
+int atta_attention_decode(void* out, float* part_out, float* part_lse, const void* q,
+                          const void* k_cache, const void* v_cache, const int* block_tables,
+                          const int* seq_kvlen, const int* seq_qstart, int num_seqs,
+                          int num_parts, int part_tokens, int n_q_heads, int n_kv_heads,
+                          int head_dim, int block_size, int bt_stride, int64_t q_stride,
+                          int64_t out_stride, float scale, int dtype, hipStream_t stream);
+
+int atta_sample(int64_t* out, const void* logits, int rows, int vocab, int64_t stride,
+                int logits_is_fp32, const float* temperature, const int64_t* seeds,
+                const int64_t* steps, hipStream_t stream);

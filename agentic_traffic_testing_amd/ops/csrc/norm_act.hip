@@ -1,0 +1,143 @@
+// Normalisation and activation kernels.
+//
+//  * rms_norm            out = x * rsqrt(mean(x^2) + eps) * w
+//  * fused_add_rms_norm  r = x + r (written back, rounded to T);  out = rmsnorm(r) * w
+//  * silu_and_mul        out[:, i] = silu(x[:, i]) * x[:, I + i]   (gate | up packed)
+//
+// These replace the per-layer norm/activation work that vLLM runs for the reference
+// (llm/serve_llm.py:527-531 -> engine.generate).  One 256-thread workgroup per row,
+// 16-byte vector loads, wave64 shuffle reduction + 4-entry LDS reduction.
+#include "common.h"
+#include "kernels.h"
+
+namespace atta {
+
+constexpr int kNormThreads = 256;
+constexpr int kNormMaxIters = 8;  // rows up to 256 * 8 * 8 = 16384 elements
+
+template <typename T, bool kAdd>
+__global__ __launch_bounds__(kNormThreads) void rms_norm_kernel(
+    uint16_t* __restrict__ out, uint16_t* __restrict__ residual, const uint16_t* __restrict__ x,
+    const uint16_t* __restrict__ w, int hidden, int64_t x_stride, int64_t out_stride,
+    int64_t res_stride, float eps) {
+  __shared__ float scratch[kNormThreads / kWave];
+  const int64_t row = blockIdx.x;
+  const int nvec = hidden >> 3;
+  const Pack8* xin = reinterpret_cast<const Pack8*>(x + row * x_stride);
+  Pack8* rrow = kAdd ? reinterpret_cast<Pack8*>(residual + row * res_stride) : nullptr;
+
+  float vals[kNormMaxIters][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int it = 0; it < kNormMaxIters; ++it) {
+    const int v = threadIdx.x + it * kNormThreads;
+    if (v < nvec) {
+      Pack8 a = xin[v];
+      if constexpr (kAdd) {
+        Pack8 r = rrow[v];
+        Pack8 s;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s.v[j] = from_f32<T>(to_f32<T>(a.v[j]) + to_f32<T>(r.v[j]));
+          vals[it][j] = to_f32<T>(s.v[j]);
+        }
+        rrow[v] = s;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vals[it][j] = to_f32<T>(a.v[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += vals[it][j] * vals[it][j];
+    }
+  }
+  ss = block_sum(ss, scratch);
+  const float inv = rsqrtf(ss / static_cast<float>(hidden) + eps);
+  const Pack8* wv = reinterpret_cast<const Pack8*>(w);
+  Pack8* o = reinterpret_cast<Pack8*>(out + row * out_stride);
+#pragma unroll
+  for (int it = 0; it < kNormMaxIters; ++it) {
+    const int v = threadIdx.x + it * kNormThreads;
+    if (v < nvec) {
+      Pack8 ww = wv[v];
+      Pack8 r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        // round the normalised value to T before the weight multiply (matches the
+        // fp32-reference definition in ops/reference.py)
+        const float n = to_f32<T>(from_f32<T>(vals[it][j] * inv));
+        r.v[j] = from_f32<T>(n * to_f32<T>(ww.v[j]));
+      }
+      o[v] = r;
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void silu_and_mul_kernel(uint16_t* __restrict__ out,
+                                                           const uint16_t* __restrict__ x,
+                                                           int inter, int64_t x_stride,
+                                                           int64_t out_stride) {
+  const int64_t row = blockIdx.y;
+  const int nvec = inter >> 3;
+  const Pack8* g = reinterpret_cast<const Pack8*>(x + row * x_stride);
+  const Pack8* u = reinterpret_cast<const Pack8*>(x + row * x_stride + inter);
+  Pack8* o = reinterpret_cast<Pack8*>(out + row * out_stride);
+  for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += gridDim.x * blockDim.x) {
+    Pack8 a = g[v], b = u[v], r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gf = to_f32<T>(a.v[j]);
+      const float s = to_f32<T>(from_f32<T>(gf / (1.f + __expf(-gf))));
+      r.v[j] = from_f32<T>(s * to_f32<T>(b.v[j]));
+    }
+    o[v] = r;
+  }
+}
+
+}  // namespace atta
+
+using namespace atta;
+
+int atta_rms_norm(void* out, void* residual, const void* x, const void* w, int rows, int hidden,
+                  int64_t x_stride, int64_t out_stride, int64_t res_stride, float eps, int dtype,
+                  hipStream_t stream) {
+  if (hidden % 8 != 0 || hidden > kNormThreads * kNormMaxIters * 8) return -1;
+  if (rows == 0) return 0;
+  dim3 grid(rows), block(kNormThreads);
+  auto o = static_cast<uint16_t*>(out);
+  auto r = static_cast<uint16_t*>(residual);
+  auto xi = static_cast<const uint16_t*>(x);
+  auto wi = static_cast<const uint16_t*>(w);
+  if (dtype == 0) {
+    if (r)
+      rms_norm_kernel<__bf16, true><<<grid, block, 0, stream>>>(o, r, xi, wi, hidden, x_stride,
+                                                                out_stride, res_stride, eps);
+    else
+      rms_norm_kernel<__bf16, false><<<grid, block, 0, stream>>>(o, r, xi, wi, hidden, x_stride,
+                                                                 out_stride, res_stride, eps);
+  } else {
+    if (r)
+      rms_norm_kernel<_Float16, true><<<grid, block, 0, stream>>>(o, r, xi, wi, hidden, x_stride,
+                                                                  out_stride, res_stride, eps);
+    else
+      rms_norm_kernel<_Float16, false><<<grid, block, 0, stream>>>(
+          o, r, xi, wi, hidden, x_stride, out_stride, res_stride, eps);
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+int atta_silu_and_mul(void* out, const void* x, int rows, int inter, int64_t x_stride,
+                      int64_t out_stride, int dtype, hipStream_t stream) {
+  if (inter % 8 != 0) return -1;
+  if (rows == 0) return 0;
+  const int nvec = inter / 8;
+  int bx = (nvec + 255) / 256;
+  dim3 grid(bx, rows), block(256);
+  if (dtype == 0)
+    silu_and_mul_kernel<__bf16><<<grid, block, 0, stream>>>(
+        static_cast<uint16_t*>(out), static_cast<const uint16_t*>(x), inter, x_stride, out_stride);
+  else
+    silu_and_mul_kernel<_Float16><<<grid, block, 0, stream>>>(
+        static_cast<uint16_t*>(out), static_cast<const uint16_t*>(x), inter, x_stride, out_stride);
+  return static_cast<int>(hipGetLastError());
+}

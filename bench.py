@@ -1,0 +1,156 @@
+#!/usr/bin/env python3
+"""Headline benchmark: llm-backend tokens/s + p50 TTFT under a 5-agent fan-out,
+Llama-3-8B (3.1 shape) bf16, TP=1 per engine (BASELINE.json).
+
+One timed *step* = one fan-out episode per rank (agentic_traffic_testing_amd/bench/fanout.py):
+planning request -> 5 concurrent Agent-B requests -> final synthesis request, each
+generating exactly ``--max-tokens`` (512) tokens with temperature 0.2.  With N GPUs
+(``torch.distributed.run --nproc-per-node N``) every rank is an independent engine replica
+(data-parallel serving, weak scaling) on its own GPU; the reported value is the whole-job
+completion tokens/s (sum over ranks / slowest rank's wall time).
+
+Weights are seeded random-init of the exact Llama-3.1-8B architecture and prompts are
+synthetic (no network / gated checkpoints), which ``data`` states.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+METRIC = "llm-backend tokens/sec + p50 TTFT under 5-agent fan-out, Llama-3-8B TP=1"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="meta-llama/Llama-3.1-8B-Instruct")
+    ap.add_argument("--max-tokens", type=int, default=512)
+    ap.add_argument("--fanout", type=int, default=5)
+    ap.add_argument("--max-model-len", type=int, default=4096)
+    ap.add_argument("--max-num-seqs", type=int, default=12)
+    ap.add_argument("--max-num-batched-tokens", type=int, default=8192)
+    ap.add_argument("--gpu-memory-utilization", type=float, default=0.90)
+    ap.add_argument("--dtype", default="bfloat16")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--verbose", action="store_true")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    dev = f"cuda:{torch.cuda.current_device()}"
+
+    from agentic_traffic_testing_amd.bench.fanout import FanoutWorkload
+    from agentic_traffic_testing_amd.config import EngineConfig
+    from agentic_traffic_testing_amd.engine.llm_engine import LLMEngine
+
+    cfg = EngineConfig(model=a.model, dtype=a.dtype, max_model_len=a.max_model_len,
+                       max_num_seqs=a.max_num_seqs,
+                       max_num_batched_tokens=a.max_num_batched_tokens,
+                       gpu_memory_utilization=a.gpu_memory_utilization,
+                       use_graphs=not a.no_graphs, seed=1234, device=dev)
+    t0 = time.perf_counter()
+    eng = LLMEngine(cfg)
+    eng.runner.capture_all()
+    init_s = time.perf_counter() - t0
+    wl = FanoutWorkload(eng, fanout=a.fanout, max_tokens=a.max_tokens, seed=rank)
+
+    def log(*x):
+        if a.verbose and rank == 0:
+            print(*x, file=sys.stderr, flush=True)
+
+    log(f"init {init_s:.1f}s kv_blocks={eng.runner.num_blocks} graphs={sorted(eng.runner.graphs)}")
+    for i in range(a.warmup):
+        r = wl.run_episode()
+        log(f"warmup {i}: {r.completion_tokens / r.seconds:.1f} tok/s, {r.seconds:.2f}s")
+
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    results = [wl.run_episode() for _ in range(a.steps)]
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+
+    tokens = sum(r.completion_tokens for r in results)
+    ttfts = [t for r in results for t in r.ttfts]
+    lat = [t for r in results for t in r.latencies]
+    stats = torch.tensor([elapsed, float(tokens)], dtype=torch.float64, device=dev)
+    if dist:
+        t_max = stats[0:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        tok_sum = stats[1:2].clone()
+        dist.all_reduce(tok_sum, op=dist.ReduceOp.SUM)
+        all_ttft = [None] * world
+        dist.all_gather_object(all_ttft, ttfts)
+        ttfts = [t for lst in all_ttft for t in lst]
+        elapsed, tokens = float(t_max.item()), float(tok_sum.item())
+    value = tokens / elapsed
+    if rank == 0:
+        ms = elapsed / a.steps * 1000.0
+        p50 = statistics.median(ttfts) if ttfts else None
+        srt = sorted(ttfts)
+        p95 = srt[min(len(srt) - 1, int(0.95 * len(srt)))] if srt else None
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if "bf" in a.dtype else a.dtype,
+            "data": "synthetic (agent fan-out prompts, synthetic tokenizer, seeded random-init "
+                    "Llama-3.1-8B weights)",
+            "config": {
+                "model": "Llama-3.1-8B (random-init)",
+                "global_batch": a.fanout * world,
+                "seq_len": a.max_model_len,
+                "parallelism": f"dp{world}" if world > 1 else "tp1",
+                "max_tokens": a.max_tokens,
+                "max_num_seqs": a.max_num_seqs,
+                "max_num_batched_tokens": a.max_num_batched_tokens,
+                "block_size": cfg.block_size,
+                "temperature": 0.2,
+                "hipgraphs": not a.no_graphs,
+            },
+            "p50_ttft_s": round(p50, 4) if p50 is not None else None,
+            "p95_ttft_s": round(p95, 4) if p95 is not None else None,
+            "p50_latency_s": round(statistics.median(lat), 3) if lat else None,
+            "requests_per_step_per_gpu": 2 + a.fanout,
+            "completion_tokens": int(tokens),
+            "init_s": round(init_s, 1),
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

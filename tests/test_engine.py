@@ -1,0 +1,90 @@
+"""Engine end-to-end: paged KV + prefix cache + chunked prefill + decode vs a dense oracle."""
+import numpy as np
+import pytest
+import torch
+
+from agentic_traffic_testing_amd.config import EngineConfig
+from agentic_traffic_testing_amd.engine.llm_engine import LLMEngine
+from agentic_traffic_testing_amd.engine.sequence import SamplingParams
+
+from helpers import dense_logits, greedy_reference
+
+
+def _prompts(seed=0, vocab=3000):
+    rng = np.random.default_rng(seed)
+    p = [rng.integers(300, vocab, size=n).tolist() for n in (40, 70, 17, 1)]
+    p.append(p[1][:50] + [5, 6, 7])  # shares a 3-block prefix with p[1]
+    return p
+
+
+def _check(eng, prompts, n=6, tol_logit=None):
+    sp = SamplingParams(temperature=0.0, max_tokens=n, ignore_eos=True)
+    outs = eng.generate(prompts, sp)
+    assert len(outs) == len(prompts)
+    m = eng.runner.model
+    bad = 0
+    for p, o in zip(prompts, outs):
+        exp = greedy_reference(m, p, n)
+        if o.token_ids != exp:
+            # allow divergence only where the oracle's top-2 logits are a near tie
+            ids = list(p)
+            for got_t, exp_t in zip(o.token_ids, exp):
+                if got_t != exp_t:
+                    lg = dense_logits(m, ids)
+                    top = torch.topk(lg, 2).values
+                    assert float(top[0] - lg[got_t]) < (tol_logit or 0.05), (o.token_ids, exp)
+                    bad += 1
+                    break
+                ids.append(got_t)
+    return outs, bad
+
+
+def test_engine_cpu_matches_dense():
+    cfg = EngineConfig(model="tiny", device="cpu", max_model_len=256, num_kv_blocks=64,
+                       max_num_batched_tokens=64, max_num_seqs=4, use_graphs=False)
+    eng = LLMEngine(cfg)
+    outs, _ = _check(eng, _prompts())
+    assert outs[-1].cached_prompt_tokens == 48  # prefix cache hit on the shared prefix
+    info = eng.kv_cache_info()
+    assert info["free_blocks"] == info["num_gpu_blocks"]  # everything released
+
+
+def test_engine_cpu_preemption():
+    """A tiny KV pool forces preemption/recompute; outputs must stay exact."""
+    cfg = EngineConfig(model="tiny", device="cpu", max_model_len=128, num_kv_blocks=16,
+                       max_num_batched_tokens=128, max_num_seqs=4, use_graphs=False,
+                       enable_prefix_caching=False)
+    eng = LLMEngine(cfg)
+    rng = np.random.default_rng(3)
+    prompts = [rng.integers(300, 3000, size=60).tolist() for _ in range(3)]
+    _check(eng, prompts, n=40)
+    assert eng.scheduler.num_preemptions > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graphs", [False, True])
+def test_engine_gpu_matches_dense(graphs):
+    cfg = EngineConfig(model="small", device="cuda", max_model_len=512, num_kv_blocks=512,
+                       max_num_batched_tokens=96, max_num_seqs=8, use_graphs=graphs,
+                       graph_batch_sizes=(1, 2, 4, 8))
+    eng = LLMEngine(cfg)
+    outs, bad = _check(eng, _prompts(vocab=30000), n=8, tol_logit=0.25)
+    assert bad <= 1
+    if graphs:
+        assert eng.runner.graph_steps > 0
+    assert outs[-1].cached_prompt_tokens == 48
+
+
+@pytest.mark.gpu
+def test_graph_replay_equals_eager():
+    """Same seeds, same prompts: hipGraph decode == eager decode token-for-token."""
+    res = []
+    for graphs in (False, True):
+        cfg = EngineConfig(model="small", device="cuda", max_model_len=512, num_kv_blocks=512,
+                           max_num_seqs=8, use_graphs=graphs, graph_batch_sizes=(1, 2, 4, 8))
+        eng = LLMEngine(cfg)
+        sp = [SamplingParams(temperature=0.7, max_tokens=12, ignore_eos=True, seed=100 + i)
+              for i in range(5)]
+        outs = eng.generate(_prompts(vocab=30000), sp)
+        res.append([o.token_ids for o in outs])
+    assert res[0] == res[1]

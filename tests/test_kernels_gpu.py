@@ -1,0 +1,210 @@
+"""HIP kernel numerics vs the fp32 PyTorch reference (ops/reference.py)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from agentic_traffic_testing_amd import ops
+from agentic_traffic_testing_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DT = [torch.bfloat16, torch.float16]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    assert ops.native_available(), ops._load_error
+
+
+def close(a, b, atol, rtol=0.0):
+    a, b = a.float(), b.float()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    assert bool((err <= tol).all()), f"max err {err.max().item():.4g}"
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("shape", [(1, 4096), (7, 4096), (33, 8192), (300, 1024), (5, 3072)])
+def test_rms_norm(dtype, shape):
+    torch.manual_seed(0)
+    x = torch.randn(shape, dtype=dtype, device="cuda")
+    w = (torch.rand(shape[1], device="cuda") + 0.5).to(dtype)
+    close(ops.rms_norm(x, w, 1e-5), ref.rms_norm(x, w, 1e-5), 2e-2, 1e-2)
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("shape", [(1, 4096), (9, 4096), (128, 8192)])
+def test_fused_add_rms_norm(dtype, shape):
+    torch.manual_seed(1)
+    x = torch.randn(shape, dtype=dtype, device="cuda")
+    r = torch.randn(shape, dtype=dtype, device="cuda")
+    w = (torch.rand(shape[1], device="cuda") + 0.5).to(dtype)
+    exp_n, exp_r = ref.fused_add_rms_norm(x, r, w, 1e-5)
+    r2 = r.clone()
+    got = ops.fused_add_rms_norm(x, r2, w, 1e-5)
+    close(r2, exp_r, 0.0)  # residual add is exact up to the same rounding
+    close(got, exp_n, 2e-2, 1e-2)
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("shape", [(1, 28672), (13, 28672), (64, 7168)])
+def test_silu_and_mul(dtype, shape):
+    torch.manual_seed(2)
+    x = torch.randn(shape, dtype=dtype, device="cuda") * 3
+    close(ops.silu_and_mul(x), ref.silu_and_mul(x), 2e-2, 1e-2)
+
+
+def _rand_cache(nb, hkv, bs, d, dtype):
+    k = torch.randn(nb, hkv, bs, d, dtype=dtype, device="cuda")
+    v = torch.randn(nb, hkv, d, bs, dtype=dtype, device="cuda")
+    return k, v
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (8, 1), (4, 1)])
+def test_rope_cache(dtype, hq, hkv):
+    torch.manual_seed(3)
+    T, D, bs, nb = 37, 128, 16, 64
+    qkv = torch.randn(T, (hq + 2 * hkv) * D, dtype=dtype, device="cuda")
+    pos = torch.randint(0, 4000, (T,), dtype=torch.int32, device="cuda")
+    slots = torch.randperm(nb * bs, device="cuda")[:T].to(torch.int32)
+    slots[5] = -1
+    cs = ref.rope_cos_sin(D, 8192, 500000.0, {"rope_type": "llama3", "factor": 8.0,
+                                              "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                                              "original_max_position_embeddings": 8192},
+                          device="cuda")
+    k1, v1 = _rand_cache(nb, hkv, bs, D, dtype)
+    k2, v2 = k1.clone(), v1.clone()
+    q_exp = ref.rope_cache(qkv, pos, slots, cs, k1, v1, hq, hkv, D)
+    q_got = ops.rope_cache(qkv, pos, slots, cs, k2, v2, hq, hkv, D)
+    close(q_got, q_exp, 2e-2, 1e-2)
+    close(k2, k1, 2e-2, 1e-2)
+    close(v2, v1, 0.0)
+
+
+def _make_paged(seqs, hkv, bs, dtype, nb_extra=8, seed=0):
+    """seqs: list of (kvlen, qlen). Returns caches, block tables, metadata on cuda."""
+    g = torch.Generator().manual_seed(seed)
+    nblk = [math.ceil(kv / bs) for kv, _ in seqs]
+    nb = sum(nblk) + nb_extra
+    perm = torch.randperm(nb, generator=g)
+    W = max(nblk) + 2
+    bt = torch.zeros(len(seqs), W, dtype=torch.int32)
+    o = 0
+    for i, n in enumerate(nblk):
+        bt[i, :n] = perm[o:o + n].to(torch.int32)
+        bt[i, n:] = -7 if i % 2 else 0  # garbage past the end must never be read
+        o += n
+    k, v = _rand_cache(nb, hkv, bs, 128, dtype)
+    kvlen = torch.tensor([kv for kv, _ in seqs], dtype=torch.int32)
+    qlens = [q for _, q in seqs]
+    qstart = torch.tensor([0] + list(np.cumsum(qlens)), dtype=torch.int32)
+    return k, v, bt.cuda(), kvlen.cuda(), qstart.cuda(), int(sum(qlens))
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 1), (4, 1), (16, 16)])
+@pytest.mark.parametrize("bs", [16, 32])
+def test_attention_prefill(dtype, hq, hkv, bs):
+    torch.manual_seed(4)
+    # (kvlen, qlen): full prompt, chunk after cached prefix, single token, long-ish
+    seqs = [(53, 53), (300, 77), (17, 1), (640, 640), (129, 2)]
+    k, v, bt, kvlen, qstart, T = _make_paged(seqs, hkv, bs, dtype)
+    q = torch.randn(T, hq, 128, dtype=dtype, device="cuda")
+    tile = ops.PREFILL_TILE_TOKENS[hq // hkv]
+    ts, to = [], []
+    for i, (_, ql) in enumerate(seqs):
+        for off in range(0, ql, tile):
+            ts.append(i)
+            to.append(off)
+    ts = torch.tensor(ts, dtype=torch.int32, device="cuda")
+    to = torch.tensor(to, dtype=torch.int32, device="cuda")
+    scale = 1 / math.sqrt(128)
+    bt_ref = bt.clamp(min=0)
+    exp = ref.paged_attention(q, k, v, bt_ref, kvlen, qstart, scale)
+    got = ops.attention_prefill(q, k, v, bt, kvlen, qstart, ts, to, scale)
+    close(got, exp, 1.5e-2, 2e-2)
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 1), (4, 1)])
+@pytest.mark.parametrize("parts", [1, 4, 16])
+def test_attention_decode(dtype, hq, hkv, parts):
+    torch.manual_seed(5)
+    bs = 16
+    seqs = [(1, 1), (17, 1), (256, 1), (1000, 1), (63, 1), (2048, 1)]
+    k, v, bt, kvlen, qstart, T = _make_paged(seqs, hkv, bs, dtype)
+    q = torch.randn(T, hq, 128, dtype=dtype, device="cuda")
+    part_tokens = 64 * math.ceil(2048 / parts / 64) if parts > 1 else 2048
+    nparts = math.ceil(2048 / part_tokens)
+    po = torch.empty(len(seqs) * hkv * nparts * 16 * 128, device="cuda")
+    pl = torch.empty(len(seqs) * hkv * nparts * 16, device="cuda")
+    scale = 1 / math.sqrt(128)
+    exp = ref.paged_attention(q, k, v, bt.clamp(min=0), kvlen, qstart, scale)
+    got = ops.attention_decode(q, k, v, bt, kvlen, qstart, scale, po, pl, nparts, part_tokens)
+    close(got, exp, 1.5e-2, 2e-2)
+
+
+def test_attention_decode_padded_and_subset():
+    """Dummy (kvlen 0) sequences and num_seqs < S must not touch other rows."""
+    dtype = torch.bfloat16
+    seqs = [(40, 1), (90, 1), (1, 1)]
+    k, v, bt, kvlen, qstart, T = _make_paged(seqs, 8, 16, dtype)
+    kvlen[2] = 0
+    q = torch.randn(T, 32, 128, dtype=dtype, device="cuda")
+    out = torch.full_like(q, 7.0)
+    po = torch.empty(3 * 8 * 4 * 16 * 128, device="cuda")
+    pl = torch.empty(3 * 8 * 4 * 16, device="cuda")
+    ops.attention_decode(q, k, v, bt, kvlen, qstart, 0.088, po, pl, 4, 64, out=out, num_seqs=1)
+    exp = ref.paged_attention(q, k, v, bt, kvlen, qstart, 0.088)
+    close(out[0], exp[0], 1.5e-2, 2e-2)
+    assert bool((out[1:] == 7.0).all())
+    ops.attention_decode(q, k, v, bt, kvlen, qstart, 0.088, po, pl, 4, 64, out=out)
+    assert bool((out[2] == 0).all())
+
+
+def test_attention_softmax_spike():
+    """A huge score on one key forces the running max to jump mid-sequence."""
+    dtype = torch.bfloat16
+    seqs = [(700, 700)]
+    k, v, bt, kvlen, qstart, T = _make_paged(seqs, 8, 16, dtype)
+    q = torch.randn(T, 32, 128, dtype=dtype, device="cuda") * 0.1
+    page = int(bt[0, 500 // 16])
+    k[page, :, 500 % 16, :] = 6.0
+    q[600:, :, :] = 1.0
+    tiles = torch.arange(0, 700, 16, dtype=torch.int32, device="cuda")
+    ts = torch.zeros_like(tiles)
+    exp = ref.paged_attention(q, k, v, bt, kvlen, qstart, 1 / math.sqrt(128))
+    got = ops.attention_prefill(q, k, v, bt, kvlen, qstart, ts, tiles, 1 / math.sqrt(128))
+    close(got, exp, 1.5e-2, 2e-2)
+
+
+def test_sample_greedy_and_gumbel():
+    torch.manual_seed(6)
+    B, V = 6, 128256
+    logits = torch.randn(B, V, device="cuda") * 3
+    temp = torch.tensor([0.0, 0.2, 1.0, 0.0, 0.7, 2.0], device="cuda")
+    seeds = torch.arange(B, dtype=torch.int64, device="cuda") * 977 + 11
+    steps = torch.arange(B, dtype=torch.int64, device="cuda") * 3
+    got = ops.sample(logits, temp, seeds, steps).cpu()
+    exp = ref.sample(logits.cpu(), temp.cpu(), seeds.cpu(), steps.cpu())
+    assert got[0] == exp[0] and got[3] == exp[3]
+    # fast-math logs may flip near-ties; the bulk must agree
+    assert int((got == exp).sum()) >= B - 1
+    # bf16 logits path
+    got16 = ops.sample(logits.to(torch.bfloat16), temp, seeds, steps).cpu()
+    assert got16[0] == int(torch.argmax(logits[0].to(torch.bfloat16).float()))
+
+
+def test_sample_distribution():
+    """Gumbel-max draws follow softmax(logits / T)."""
+    V, N = 16, 4000
+    logits = torch.linspace(-2, 2, V, device="cuda").repeat(N, 1)
+    temp = torch.full((N,), 0.8, device="cuda")
+    seeds = torch.full((N,), 42, dtype=torch.int64, device="cuda")
+    steps = torch.arange(N, dtype=torch.int64, device="cuda")
+    toks = ops.sample(logits, temp, seeds, steps).cpu()
+    freq = torch.bincount(toks, minlength=V).float() / N
+    p = torch.softmax(logits[0].cpu() / 0.8, -1)
+    assert float((freq - p).abs().max()) < 0.03
