@@ -1,0 +1,149 @@
+"""Asyncio front for the engine: a dedicated engine thread runs the step loop, HTTP
+handlers submit requests and await streamed outputs.
+
+Mirrors the reference's use of ``AsyncLLMEngine.generate`` (an async generator yielding
+one output per engine step; llm/serve_llm.py:527-580).  Requests are handed to the
+engine thread through a lock-free deque so the event loop never blocks on a running GPU
+step; outputs come back with ``loop.call_soon_threadsafe``.
+
+Watchdog: ``heartbeat`` is refreshed every loop iteration;
+``stalled(threshold)`` is true when work is pending but the loop has not progressed for
+``threshold`` seconds, and the HTTP layer reports that on /health as 503.
+"""
+from __future__ import annotations
+
+import asyncio
+import collections
+import threading
+import time
+import traceback
+
+from .llm_engine import LLMEngine, RequestOutput
+from .sequence import SamplingParams
+
+
+class EngineDeadError(RuntimeError):
+    pass
+
+
+class AsyncEngine:
+    def __init__(self, engine: LLMEngine, on_step=None):
+        self.engine = engine
+        self.on_step = on_step
+        self._pending: collections.deque = collections.deque()
+        self._aborts: collections.deque = collections.deque()
+        self._streams: dict[str, tuple] = {}
+        self._wake = threading.Event()
+        self._stop = threading.Event()
+        self._thread: threading.Thread | None = None
+        self.heartbeat = time.monotonic()
+        self.last_error: str | None = None
+        self.fault_injection_delay_s = 0.0  # optional test hook: extra per-step delay
+
+    # ------------------------------------------------------------------------------------
+    def start(self):
+        if self._thread is None:
+            self._thread = threading.Thread(target=self._run, name="engine-loop", daemon=True)
+            self._thread.start()
+        return self
+
+    def shutdown(self):
+        self._stop.set()
+        self._wake.set()
+        if self._thread is not None:
+            self._thread.join(timeout=10)
+
+    def stalled(self, threshold_s: float = 60.0) -> bool:
+        busy = bool(self._pending) or self.engine.has_unfinished()
+        return busy and (time.monotonic() - self.heartbeat) > threshold_s
+
+    @property
+    def alive(self) -> bool:
+        return self._thread is not None and self._thread.is_alive()
+
+    # ------------------------------------------------------------------------------------
+    async def generate(self, prompt_ids, sampling: SamplingParams, request_id: str):
+        """Async generator of RequestOutput (one per engine step that produced a token)."""
+        if not self.alive:
+            raise EngineDeadError("engine loop is not running")
+        loop = asyncio.get_running_loop()
+        q: asyncio.Queue = asyncio.Queue()
+        self._streams[request_id] = (loop, q)
+        self._pending.append((request_id, list(prompt_ids), sampling, time.perf_counter()))
+        self._wake.set()
+        done = False
+        try:
+            while True:
+                item = await q.get()
+                if isinstance(item, BaseException):
+                    done = True
+                    raise item
+                done = item.finished
+                yield item
+                if done:
+                    return
+        finally:
+            self._streams.pop(request_id, None)
+            if not done:  # consumer went away (client disconnect / cancel): free the slot
+                self._aborts.append(request_id)
+                self._wake.set()
+
+    async def generate_full(self, prompt_ids, sampling: SamplingParams,
+                            request_id: str) -> tuple[RequestOutput, float]:
+        """Run to completion. Returns (final output, TTFT seconds)."""
+        t0 = time.perf_counter()
+        ttft = None
+        final = None
+        async for out in self.generate(prompt_ids, sampling, request_id):
+            if ttft is None:
+                ttft = time.perf_counter() - t0
+            final = out
+        return final, (ttft or 0.0)
+
+    # ------------------------------------------------------------------------------------
+    def _deliver(self, rid: str, item):
+        s = self._streams.get(rid)
+        if s is None:
+            return
+        loop, q = s
+        try:
+            loop.call_soon_threadsafe(q.put_nowait, item)
+        except RuntimeError:  # loop closed
+            pass
+
+    def _run(self):
+        eng = self.engine
+        while not self._stop.is_set():
+            self.heartbeat = time.monotonic()
+            while self._pending:
+                rid, ids, sp, t_arr = self._pending.popleft()
+                try:
+                    eng.add_request(rid, ids, sp, arrival_time=t_arr)
+                except Exception as e:  # bad request: fail only that one
+                    self._deliver(rid, e)
+            while self._aborts:
+                eng.abort(self._aborts.popleft())
+            if not eng.has_unfinished():
+                self._wake.wait(0.05)
+                self._wake.clear()
+                continue
+            try:
+                t0 = time.perf_counter()
+                outs = eng.step()
+                if self.fault_injection_delay_s:
+                    time.sleep(self.fault_injection_delay_s)
+                if self.on_step is not None and eng.last_step is not None:
+                    try:
+                        self.on_step(eng.last_step, time.perf_counter() - t0)
+                    except Exception:
+                        pass
+            except Exception as e:
+                self.last_error = "".join(traceback.format_exception(e))[-2000:]
+                err = RuntimeError(f"engine step failed: {e}")
+                # fail every in-flight request; keep the loop alive for new ones
+                for s in list(eng.scheduler.running) + list(eng.scheduler.waiting):
+                    eng.abort(s.request_id)
+                    self._deliver(s.request_id, err)
+                continue
+            for o in outs:
+                self._deliver(o.request_id, o)

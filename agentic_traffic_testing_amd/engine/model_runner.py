@@ -16,6 +16,7 @@ One step = one forward over a decode-first ``Batch`` (scheduler.py) followed by 
 from __future__ import annotations
 
 import math
+import os
 import time
 
 import numpy as np
@@ -152,7 +153,7 @@ class ModelRunner:
             budget = total * self.cfg.gpu_memory_utilization - used - act
             nb = int(budget // per_block)
         else:
-            nb = 256
+            nb = int(os.environ.get("ATTA_CPU_KV_BLOCKS", "256"))
         nb = max(nb, 2 * self.bt_width)
         self.num_blocks = nb
         shape_k = (L, nb, m.n_kv_heads, self.block_size, m.head_dim)

@@ -106,6 +106,7 @@ __global__ __launch_bounds__(256) void paged_attention_kernel(AttnParams p) {
   const int qstart = p.seq_qstart[s];
   const int qlen = p.seq_qstart[s + 1] - qstart;
   const int ctx0 = kvlen - qlen;  // position of the first query token
+  if (qlen <= 0) return;          // block-uniform: nothing to compute for this sequence
 
   // ---- this lane's column: (token, head) --------------------------------------------
   const int c_tok = kSplitKV ? (qlen - 1) : (qoff + col / G);

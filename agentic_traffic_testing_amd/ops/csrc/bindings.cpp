@@ -8,7 +8,7 @@
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <c10/core/DeviceGuard.h>
 
 #include "kernels.h"
 
@@ -33,7 +33,7 @@ void check_dev(const at::Tensor& t, const char* name) {
 void rms_norm(at::Tensor out, const at::Tensor& x, const at::Tensor& w, double eps) {
   check_dev(x, "x");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && out.stride(1) == 1, "rms_norm: 2-D rows");
-  c10::hip::HIPGuard g(x.device());
+  const at::DeviceGuard g(x.device());
   check_rc(atta_rms_norm(out.data_ptr(), nullptr, x.data_ptr(), w.data_ptr(), x.size(0),
                          x.size(1), x.stride(0), out.stride(0), 0, static_cast<float>(eps),
                          dtype_code(x), cur_stream()),
@@ -46,7 +46,7 @@ void fused_add_rms_norm(at::Tensor out, at::Tensor residual, const at::Tensor& x
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && residual.stride(1) == 1 && out.stride(1) == 1,
               "fused_add_rms_norm: 2-D rows");
   TORCH_CHECK(residual.sizes() == x.sizes(), "fused_add_rms_norm: residual shape");
-  c10::hip::HIPGuard g(x.device());
+  const at::DeviceGuard g(x.device());
   check_rc(atta_rms_norm(out.data_ptr(), residual.data_ptr(), x.data_ptr(), w.data_ptr(),
                          x.size(0), x.size(1), x.stride(0), out.stride(0), residual.stride(0),
                          static_cast<float>(eps), dtype_code(x), cur_stream()),
@@ -57,7 +57,7 @@ void silu_and_mul(at::Tensor out, const at::Tensor& x) {
   check_dev(x, "x");
   TORCH_CHECK(x.dim() == 2 && x.size(1) % 2 == 0 && x.stride(1) == 1, "silu_and_mul: x");
   TORCH_CHECK(out.size(1) * 2 == x.size(1) && out.size(0) == x.size(0), "silu_and_mul: out");
-  c10::hip::HIPGuard g(x.device());
+  const at::DeviceGuard g(x.device());
   check_rc(atta_silu_and_mul(out.data_ptr(), x.data_ptr(), x.size(0), out.size(1), x.stride(0),
                              out.stride(0), dtype_code(x), cur_stream()),
            "silu_and_mul");
@@ -78,7 +78,7 @@ void rope_cache(at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache, const 
               "rope_cache: k_cache [nb, Hkv, BS, D]");
   TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(2) == head_dim, "rope_cache: v_cache [nb,Hkv,D,BS]");
   const int64_t q_out_stride = q_out.dim() == 3 ? q_out.stride(0) : q_out.stride(0);
-  c10::hip::HIPGuard g(qkv.device());
+  const at::DeviceGuard g(qkv.device());
   check_rc(atta_rope_cache(q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                            qkv.data_ptr(), positions.data_ptr<int>(),
                            slot_mapping.data_ptr<int>(), cos_sin.data_ptr<float>(),
@@ -98,7 +98,7 @@ void attention_prefill(at::Tensor out, const at::Tensor& q, const at::Tensor& k_
                   tile_qoff.scalar_type() == at::kInt,
               "attention_prefill: metadata must be int32");
   TORCH_CHECK(q.stride(-1) == 1 && out.stride(-1) == 1, "attention_prefill: last dim contiguous");
-  c10::hip::HIPGuard g(q.device());
+  const at::DeviceGuard g(q.device());
   check_rc(atta_attention_prefill(
                out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                block_tables.data_ptr<int>(), seq_kvlen.data_ptr<int>(), seq_qstart.data_ptr<int>(),
@@ -124,7 +124,7 @@ void attention_decode(at::Tensor out, at::Tensor part_out, at::Tensor part_lse,
                     part_lse.numel() >= num_seqs * n_kv_heads * num_parts * 16,
                 "attention_decode: partition workspace too small");
   }
-  c10::hip::HIPGuard g(q.device());
+  const at::DeviceGuard g(q.device());
   check_rc(atta_attention_decode(
                out.data_ptr(), part_out.data_ptr<float>(), part_lse.data_ptr<float>(),
                q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
@@ -144,7 +144,7 @@ void sample(at::Tensor out, const at::Tensor& logits, const at::Tensor& temperat
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "sample: logits 2-D");
   const bool is_f32 = logits.scalar_type() == at::kFloat;
   TORCH_CHECK(is_f32 || logits.scalar_type() == at::kBFloat16, "sample: logits fp32/bf16");
-  c10::hip::HIPGuard g(logits.device());
+  const at::DeviceGuard g(logits.device());
   check_rc(atta_sample(out.data_ptr<int64_t>(), logits.data_ptr(), logits.size(0),
                        logits.size(1), logits.stride(0), is_f32 ? 1 : 0,
                        temperature.data_ptr<float>(), seeds.data_ptr<int64_t>(),

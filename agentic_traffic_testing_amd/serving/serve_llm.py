@@ -1,0 +1,427 @@
+"""LLM backend HTTP server (``python -m llm.serve_llm``) on the MI355X-native engine.
+
+API-compatible with the reference's aiohttp front end over vLLM (llm/serve_llm.py):
+
+* ``POST /chat | /completion | /generate`` with ``{prompt|input, max_tokens?, request_id?,
+  system_prompt?, skip_chat_template?}`` -> ``{"output", "meta": {request_id, latency_ms,
+  queue_wait_s, prompt_tokens, completion_tokens, total_tokens, otel}}``; 400 on bad JSON /
+  missing prompt, 503 before init, 500 ``Generation failed: ...`` (serve_llm.py:731-942);
+* ``GET /health | /ready | /live`` -> ``{"status": "ok"}``; ``GET /metrics`` -> Prometheus
+  text of the exact ``llm_*`` families (serving/metrics.py);
+* the same stdout line protocol (``[llm] req=<id> START/PROGRESS/GENERATED/DONE/ERROR``),
+  Llama-3 chat templating and head-keeping prompt truncation
+  (``max(0, LLM_MAX_MODEL_LEN - max_new - LLM_PROMPT_SAFETY_MARGIN_TOKENS)``);
+* the same CLI flags and env fallbacks (serve_llm.py:1050-1104).
+
+Differences, by design: ``queue_wait_s`` is the engine-measured TTFT (submission -> first
+token, incl. prefill, like the reference); ``completion_tokens`` is the engine's token count
+(the reference re-tokenises the output text, serve_llm.py:881-882 - ``meta`` also carries
+``completion_tokens_text`` for that definition); /health turns 503 when the engine loop has
+stalled with work pending (watchdog).  Extra flags: ``--tensor-parallel-size``,
+``--block-size``, ``--no-prefix-caching``, ``--no-graphs``, ``--load-format``.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import sys
+import time
+import uuid
+
+from aiohttp import web
+
+from ..engine.sequence import SamplingParams
+from ..engine.tokenizer import apply_chat_template
+from ..utils import otel
+from .metrics import CONTENT_TYPE_LATEST, LLMMetrics
+
+
+def _env_bool(name: str, default: str) -> bool:
+    return os.environ.get(name, default).lower() in ("1", "true", "yes", "on")
+
+
+class Settings:
+    def __init__(self):
+        e = os.environ
+        self.model = e.get("LLM_MODEL", "meta-llama/Llama-3.1-8B-Instruct")
+        self.log_requests = _env_bool("LOG_LLM_REQUESTS", "")
+        self.log_max_chars = int(e.get("LLM_LOG_MAX_CHARS", "500"))
+        self.max_tokens = int(e.get("LLM_MAX_TOKENS", "512"))
+        self.max_model_len_env = int(e.get("LLM_MAX_MODEL_LEN") or "0")
+        self.margin = int(e.get("LLM_PROMPT_SAFETY_MARGIN_TOKENS", "128"))
+        self.metrics_enabled = _env_bool("LLM_METRICS_ENABLED", "1")
+        self.metrics_prefix = e.get("LLM_METRICS_PREFIX", "llm")
+        self.apply_template = _env_bool("LLM_APPLY_CHAT_TEMPLATE", "1")
+        self.temperature = float(e.get("LLM_TEMPERATURE", "0.2"))
+        self.watchdog_s = float(e.get("LLM_WATCHDOG_SECONDS", "120"))
+
+
+class ServerState:
+    def __init__(self, engine, async_engine, settings: Settings | None = None,
+                 metrics: LLMMetrics | None = None, model_name: str = ""):
+        self.engine = engine
+        self.aengine = async_engine
+        self.s = settings or Settings()
+        self.metrics = metrics if metrics is not None else (
+            LLMMetrics(self.s.metrics_prefix) if self.s.metrics_enabled else None)
+        self.tracer = otel.get_tracer("llm-backend")
+        self.inflight = 0
+        self.last_arrival: float | None = None
+        self.model_name = model_name
+        self.tok = engine.tokenizer if engine is not None else None
+
+    def log(self, msg: str):
+        print(msg, flush=True)
+
+    # ----------------------------------------------------------------------------------
+    def export_config(self):
+        m, cfg = self.metrics, self.engine.cfg
+        if m is None:
+            return
+        m.cfg_max_num_seqs.set(float(cfg.max_num_seqs))
+        m.cfg_max_num_batched_tokens.set(float(cfg.max_num_batched_tokens))
+        m.cfg_gpu_mem_util.set(float(cfg.gpu_memory_utilization))
+        m.cfg_max_tokens.set(float(self.s.max_tokens))
+        info = self.engine.kv_cache_info()
+        m.set_kv(info["num_gpu_blocks"], info["block_size"], cfg.max_model_len)
+        self.log(f"[llm-metrics] KV cache gauges set at startup: num_gpu_blocks="
+                 f"{info['num_gpu_blocks']} block_size={info['block_size']} max_model_len="
+                 f"{cfg.max_model_len} total_tokens={info['total_tokens']} est_max_concurrency="
+                 f"{info['total_tokens'] // max(1, cfg.max_model_len)}")
+
+    def on_step(self, stats, seconds: float):
+        m = self.metrics
+        if m is None:
+            return
+        m.batch_size.observe(stats.num_seqs)
+        m.engine_steps.inc()
+        m.engine_step_seconds.observe(seconds)
+
+    def refresh_gauges(self):
+        m = self.metrics
+        if m is None or self.engine is None:
+            return
+        sch = self.engine.scheduler
+        m.engine_running.set(len(sch.running))
+        m.engine_waiting.set(len(sch.waiting))
+        info = self.engine.kv_cache_info()
+        m.kv_free_blocks.set(info["free_blocks"])
+        m.prefix_hits.set(info["prefix_hits"])
+        m.prefix_queries.set(info["prefix_queries"])
+        if self.aengine is not None:
+            m.heartbeat_age.set(max(0.0, time.monotonic() - self.aengine.heartbeat))
+
+
+def _log_prompt(st: ServerState, source: str, prompt: str):
+    if not st.s.log_requests:
+        return
+    n = max(st.s.log_max_chars, 0)
+    preview = prompt[:n] if n else ""
+    suffix = "" if len(prompt) <= n else f"... [truncated {len(prompt) - n} chars]"
+    st.log(f"[llm-request] source={source} prompt_len={len(prompt)} prompt={preview}{suffix}")
+
+
+async def handle_health(request: web.Request) -> web.Response:
+    st: ServerState = request.app["state"]
+    if st.aengine is not None and (not st.aengine.alive or st.aengine.stalled(st.s.watchdog_s)):
+        return web.json_response({"status": "unhealthy", "reason": "engine loop stalled"},
+                                 status=503)
+    return web.json_response({"status": "ok"})
+
+
+async def handle_metrics(request: web.Request) -> web.Response:
+    st: ServerState = request.app["state"]
+    if st.metrics is None:
+        return web.json_response({"error": "Metrics disabled"}, status=503)
+    st.refresh_gauges()
+    return web.Response(body=st.metrics.exposition(), headers={"Content-Type": CONTENT_TYPE_LATEST})
+
+
+async def handle_chat(request: web.Request) -> web.Response:
+    st: ServerState = request.app["state"]
+    if st.engine is None or st.aengine is None:
+        return web.json_response({"error": "Backend not initialized"}, status=503)
+    ctx = otel.extract(dict(request.headers))
+    with st.tracer.start_as_current_span("llm.handle_request", context=ctx,
+                                         kind=otel.SpanKind.SERVER) as span:
+        start = time.monotonic()
+        if st.last_arrival is not None and st.metrics is not None:
+            st.metrics.interarrival.observe(start - st.last_arrival)
+        st.last_arrival = start
+        st.inflight += 1
+        current_inflight = st.inflight
+        if st.metrics:
+            st.metrics.inflight.inc()
+        span.set_attribute("app.path", request.path)
+
+        def _leave():
+            st.inflight -= 1
+            if st.metrics:
+                st.metrics.inflight.dec()
+            return st.inflight
+
+        try:
+            data = await request.json()
+            if not isinstance(data, dict):
+                raise json.JSONDecodeError("not an object", "", 0)
+        except (json.JSONDecodeError, UnicodeDecodeError, ValueError):
+            _leave()
+            return web.json_response({"error": "Invalid JSON"}, status=400)
+        prompt = data.get("prompt") or data.get("input")
+        if not isinstance(prompt, str) or not prompt:
+            _leave()
+            return web.json_response({"error": "Missing 'prompt' field"}, status=400)
+        max_tokens = data.get("max_tokens")
+        if max_tokens is not None and not isinstance(max_tokens, int):
+            try:
+                max_tokens = int(max_tokens)
+            except (TypeError, ValueError):
+                max_tokens = None
+        rid = request.headers.get("X-Request-ID") or data.get("request_id")
+        request_id = str(rid) if rid else str(uuid.uuid4())[:8]
+        span.set_attribute("app.request_id", request_id)
+
+        original = prompt
+        skip = bool(data.get("skip_chat_template", False))
+        templated = (not skip) and st.s.apply_template
+        if templated:
+            prompt = apply_chat_template(prompt, data.get("system_prompt"))
+        ids = st.tok.encode(prompt)
+        eff_new = max_tokens if max_tokens is not None else st.s.max_tokens
+        truncated_tokens = None
+        mml = st.s.max_model_len_env
+        if mml > 0:
+            keep = max(0, mml - eff_new - st.s.margin)
+            if len(ids) > keep:
+                truncated_tokens = len(ids) - keep
+                st.log(f"[llm] req={request_id} PROMPT_TRUNCATED original_tokens={len(ids)} "
+                       f"kept={keep} dropped={truncated_tokens}")
+                ids = ids[:keep]
+        span.set_attribute("app.prompt_length", len(original))
+        span.set_attribute("app.formatted_prompt_length", len(prompt))
+        span.set_attribute("app.chat_template_applied", templated)
+        span.set_attribute("app.prompt_truncated", truncated_tokens is not None)
+        if truncated_tokens is not None:
+            span.set_attribute("app.prompt_truncated_tokens", int(truncated_tokens))
+        if st.s.log_requests:
+            span.set_attribute("app.prompt_preview", original[:200])
+        _log_prompt(st, "http", original)
+        tinfo = " (templated)" if templated else ""
+        trunc = f" [TRUNCATED -{truncated_tokens}tok]" if truncated_tokens else ""
+        st.log(f"[llm] req={request_id} START inflight={current_inflight} "
+               f"prompt_len={len(original)}{tinfo}{trunc}")
+
+        sp = SamplingParams(temperature=float(data.get("temperature", st.s.temperature)),
+                            max_tokens=max(1, eff_new), ignore_eos=bool(data.get("ignore_eos", False)),
+                            seed=data.get("seed"))
+        queue_wait = 0.0
+        final = None
+        try:
+            wait_span = st.tracer.start_span("llm.time_to_first_token")
+            gen_span = None
+            t_sub = time.monotonic()
+            last_log = t_sub
+            async for out in st.aengine.generate(ids, sp, request_id):
+                if gen_span is None:
+                    queue_wait = time.monotonic() - t_sub
+                    wait_span.set_attribute("llm_ttft_seconds", queue_wait)
+                    wait_span.end()
+                    gen_span = st.tracer.start_span("llm.generate")
+                    gen_span.set_attribute("app.request_id", request_id)
+                    t_first = time.monotonic()
+                final = out
+                now = time.monotonic()
+                if now - last_log >= 2.0:
+                    el = now - t_sub
+                    st.log(f"[llm] req={request_id} PROGRESS tokens={len(out.token_ids)} "
+                           f"speed={len(out.token_ids) / el if el > 0 else 0:.1f} tok/s")
+                    last_log = now
+            if wait_span.is_recording():
+                wait_span.end()
+            text = st.tok.decode(final.token_ids) if final is not None else ""
+            el = time.monotonic() - t_sub
+            ntok = len(final.token_ids) if final is not None else 0
+            st.log(f"[llm] req={request_id} GENERATED tokens={ntok} time={el:.2f}s "
+                   f"speed={ntok / el if el > 0 else 0:.1f} tok/s")
+            if gen_span is not None:
+                gen_span.set_attribute("llm.generate_ms", int((time.monotonic() - t_first) * 1000))
+                gen_span.end()
+            prompt_tokens = len(ids)
+            completion_tokens = ntok
+            span.set_attribute("llm.prompt_tokens", prompt_tokens)
+            span.set_attribute("llm.completion_tokens", completion_tokens)
+            span.set_attribute("llm.total_tokens", prompt_tokens + completion_tokens)
+        except Exception as exc:
+            _leave()
+            lat = time.monotonic() - start
+            st.log(f"[llm] req={request_id} ERROR after {int(lat * 1000)}ms: {exc}")
+            if st.metrics:
+                st.metrics.record("error", lat, queue_wait, None, None)
+            return web.json_response({"error": f"Generation failed: {exc}"}, status=500)
+
+        remaining = _leave()
+        lat = time.monotonic() - start
+        latency_ms = int(lat * 1000)
+        st.log(f"[llm] req={request_id} DONE latency={latency_ms}ms prompt={prompt_tokens} "
+               f"completion={completion_tokens} remaining={remaining}")
+        if st.metrics:
+            st.metrics.record("success", lat, queue_wait, prompt_tokens, completion_tokens)
+            st.metrics.ttft.observe(queue_wait)
+        if st.s.log_requests:
+            st.log(f"[llm-metrics] status=success latency_ms={latency_ms} prompt_tokens="
+                   f"{prompt_tokens} completion_tokens={completion_tokens}")
+        meta = {
+            "request_id": request_id,
+            "latency_ms": latency_ms,
+            "queue_wait_s": round(queue_wait, 4),
+            "prompt_tokens": prompt_tokens,
+            "completion_tokens": completion_tokens,
+            "total_tokens": prompt_tokens + completion_tokens,
+            "otel": otel.span_metadata(span),
+            "ttft_s": round(queue_wait, 6),
+            "cached_prompt_tokens": final.cached_prompt_tokens if final else 0,
+            "finish_reason": final.finish_reason if final else None,
+            "completion_tokens_text": st.tok.count(text),
+        }
+        return web.json_response({"output": text, "meta": meta})
+
+
+def create_app(state: ServerState) -> web.Application:
+    app = web.Application(client_max_size=64 * 1024 * 1024)
+    app["state"] = state
+    app.router.add_get("/health", handle_health)
+    app.router.add_get("/ready", handle_health)
+    app.router.add_get("/live", handle_health)
+    app.router.add_get("/metrics", handle_metrics)
+    app.router.add_post("/chat", handle_chat)
+    app.router.add_post("/completion", handle_chat)
+    app.router.add_post("/generate", handle_chat)
+    return app
+
+
+def build_engine(args):
+    """Build the (possibly tensor-parallel) engine from CLI args + env fallbacks."""
+    from ..config import EngineConfig
+    from ..engine.llm_engine import LLMEngine
+
+    kw = dict(model=args.model)
+    if args.max_model_len:
+        kw["max_model_len"] = args.max_model_len
+    if args.dtype:
+        kw["dtype"] = args.dtype
+    if args.max_num_seqs:
+        kw["max_num_seqs"] = args.max_num_seqs
+    if args.max_num_batched_tokens:
+        kw["max_num_batched_tokens"] = args.max_num_batched_tokens
+    if args.gpu_memory_utilization:
+        kw["gpu_memory_utilization"] = args.gpu_memory_utilization
+    if args.block_size:
+        kw["block_size"] = args.block_size
+    if args.tensor_parallel_size:
+        kw["tensor_parallel_size"] = args.tensor_parallel_size
+    kw["enable_prefix_caching"] = not args.no_prefix_caching
+    kw["use_graphs"] = not args.no_graphs
+    kw["load_format"] = args.load_format
+    if args.device:
+        kw["device"] = args.device
+    cfg = EngineConfig.from_env(**kw)
+    if cfg.tensor_parallel_size > 1:
+        from ..parallel.tp_engine import TPEngine
+
+        return TPEngine(cfg)
+    eng = LLMEngine(cfg)
+    eng.runner.capture_all()
+    return eng
+
+
+async def run_server(args) -> None:
+    from ..engine.async_engine import AsyncEngine
+
+    print(f"[*] Initializing MI355X engine for {args.model}...", flush=True)
+    t0 = time.time()
+    eng = build_engine(args)
+    state = ServerState(eng, None, model_name=args.model)
+    aeng = AsyncEngine(eng, on_step=state.on_step).start()
+    state.aengine = aeng
+    state.export_config()
+    app = create_app(state)
+    runner = web.AppRunner(app, access_log=None)
+    await runner.setup()
+    site = web.TCPSite(runner, args.host, args.port)
+    cfg = eng.cfg
+    print("=" * 60)
+    print("[*] MI355X serving engine ready")
+    print(f"    Model: {args.model}")
+    print(f"    URL: http://{args.host}:{args.port}")
+    print(f"    max_num_seqs: {cfg.max_num_seqs}")
+    print(f"    max_model_len: {cfg.max_model_len}")
+    print(f"    tensor_parallel_size: {cfg.tensor_parallel_size}")
+    print(f"    KV blocks: {eng.kv_cache_info()['num_gpu_blocks']} x {cfg.block_size} tokens")
+    print(f"    init: {time.time() - t0:.1f}s")
+    print("    Batching: ENABLED (continuous batching, chunked prefill, prefix caching)")
+    print("=" * 60, flush=True)
+    await site.start()
+    try:
+        while True:
+            await asyncio.sleep(3600)
+    except asyncio.CancelledError:
+        pass
+    finally:
+        aeng.shutdown()
+        await runner.cleanup()
+
+
+def make_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="MI355X-native LLM backend for the agentic traffic testbed")
+    p.add_argument("--model", default=os.environ.get("LLM_MODEL", "meta-llama/Llama-3.1-8B-Instruct"))
+    p.add_argument("--host", default="0.0.0.0")
+    p.add_argument("--port", type=int, default=8000)
+    p.add_argument("--max-model-len", type=int, default=None)
+    p.add_argument("--dtype", default=None)
+    p.add_argument("--max-num-seqs", type=int, default=None)
+    p.add_argument("--max-num-batched-tokens", type=int, default=None)
+    p.add_argument("--gpu-memory-utilization", type=float, default=None)
+    p.add_argument("--tensor-parallel-size", "--tp-size", type=int, default=None)
+    p.add_argument("--block-size", type=int, default=None)
+    p.add_argument("--no-prefix-caching", action="store_true")
+    p.add_argument("--no-graphs", action="store_true")
+    p.add_argument("--load-format", default="auto", choices=["auto", "dummy", "safetensors"])
+    p.add_argument("--device", default=None)
+    p.add_argument("--config", default=None,
+                   help="YAML file of EngineConfig keys (e.g. llm/config/llama-3.1-8b.yaml); "
+                        "explicit flags win")
+    return p
+
+
+def apply_config_file(args):
+    if not args.config:
+        return args
+    import yaml
+
+    with open(args.config) as f:
+        data = yaml.safe_load(f) or {}
+    for key, val in data.items():
+        attr = key.replace("-", "_")
+        if attr == "enable_prefix_caching":
+            if not val:
+                args.no_prefix_caching = True
+            continue
+        if attr == "model" and args.model != make_parser().get_default("model"):
+            continue
+        if hasattr(args, attr) and getattr(args, attr) in (None, make_parser().get_default(attr)):
+            setattr(args, attr, val)
+    return args
+
+
+def main(argv=None) -> None:
+    args = apply_config_file(make_parser().parse_args(argv))
+    try:
+        asyncio.run(run_server(args))
+    except KeyboardInterrupt:
+        print("\n[*] Shutting down MI355X serving engine.")
+
+
+if __name__ == "__main__":
+    sys.exit(main())
