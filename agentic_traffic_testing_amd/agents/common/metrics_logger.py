@@ -1,0 +1,57 @@
+"""Per-LLM-call JSONL records in ``logs/llm_calls.jsonl`` (reference
+agents/common/metrics_logger.py:1-72; consumed by experiments/correlate_metrics.py).
+
+Record: call_id, task_id, agent_id, parent_call_id, call_type (root | sub_call |
+tool_call | verification), prompt_tokens, completion_tokens, total_tokens, latency_ms,
+model_name, timestamp_start, timestamp_end, http_status, error.  Token/latency fields come
+from the LLM backend's ``meta`` object.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import threading
+import uuid
+
+CALL_TYPES = ("root", "sub_call", "tool_call", "verification")
+
+
+class MetricsLogger:
+    _lock = threading.Lock()
+
+    def __init__(self, log_dir: str | None = None):
+        log_dir = log_dir or os.environ.get("METRICS_LOG_DIR", "logs")
+        os.makedirs(log_dir, exist_ok=True)
+        self.log_file = os.path.join(log_dir, "llm_calls.jsonl")
+        self.model_name = os.environ.get("MODEL_NAME", "unknown")
+
+    def log_call(self, *, task_id: str, agent_id: str, call_type: str, timestamp_start: str,
+                 timestamp_end: str, http_status: int, llm_meta: dict | None = None,
+                 error: str | None = None, parent_call_id: str | None = None,
+                 call_id: str | None = None) -> str:
+        meta = llm_meta if isinstance(llm_meta, dict) else {}
+        cid = call_id or meta.get("request_id") or str(uuid.uuid4())
+        rec = {
+            "call_id": cid,
+            "task_id": task_id,
+            "agent_id": agent_id,
+            "parent_call_id": parent_call_id,
+            "call_type": call_type,
+            "prompt_tokens": meta.get("prompt_tokens"),
+            "completion_tokens": meta.get("completion_tokens"),
+            "total_tokens": meta.get("total_tokens"),
+            "latency_ms": meta.get("latency_ms"),
+            "model_name": self.model_name,
+            "timestamp_start": timestamp_start,
+            "timestamp_end": timestamp_end,
+            "http_status": http_status,
+            "error": error,
+        }
+        line = json.dumps(rec, sort_keys=True, default=str)
+        try:
+            with self._lock, open(self.log_file, "a", encoding="utf-8") as f:
+                f.write(line + "\n")
+        except OSError as exc:
+            print(f"[metrics-logger-error] {exc}: {line}", file=sys.stderr)
+        return cid

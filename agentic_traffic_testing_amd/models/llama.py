@@ -218,7 +218,7 @@ class LlamaModel:
                 x = ops.rms_norm(h, L.input_norm, eps)
             else:
                 x = ops.fused_add_rms_norm(h, residual, L.input_norm, eps)
-            qkv = F.linear(x, L.qkv)
+            qkv = ops.linear(x, L.qkv)
             q = ops.rope_cache(qkv, md.positions, md.slot_mapping, self.cos_sin, k_caches[li],
                                v_caches[li], nq, nkv, D)
             attn = torch.empty_like(q)
@@ -230,15 +230,15 @@ class LlamaModel:
                 ops.attention_prefill(q, k_caches[li], v_caches[li], md.block_tables,
                                       md.seq_kvlen, md.seq_qstart, md.tile_seq, md.tile_qoff,
                                       self.scale, out=attn)
-            h = self._all_reduce(F.linear(attn.view(T, nq * D), L.o))
+            h = self._all_reduce(ops.linear(attn.view(T, nq * D), L.o))
             x = ops.fused_add_rms_norm(h, residual, L.post_norm, eps)
-            gu = F.linear(x, L.gate_up)
+            gu = ops.linear(x, L.gate_up)
             a = ops.silu_and_mul(gu)
-            h = self._all_reduce(F.linear(a, L.down))
+            h = self._all_reduce(ops.linear(a, L.down))
         return ops.fused_add_rms_norm(h, residual, self.norm, eps)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
-        logits = F.linear(hidden, self.lm_head)
+        logits = ops.linear(hidden, self.lm_head)
         if self.tp_size > 1:
             from ..parallel import comm
 

@@ -151,3 +151,32 @@ def sample(logits, temperature, seeds, steps, out=None):
 
 
 PREFILL_TILE_TOKENS = {1: 64, 2: 32, 4: 16, 8: 8}  # tokens per prefill workgroup by GQA group
+
+# skinny-GEMM (decode) dispatch: rows <= SKINNY_MAX_M use the MFMA weight-streaming kernel,
+# larger M (prefill) goes to hipBLASLt through F.linear.
+SKINNY_MAX_M = int(os.environ.get("ATTA_SKINNY_MAX_M", "64"))
+SKINNY_WAVES = int(os.environ.get("ATTA_SKINNY_WAVES", "4"))
+
+
+def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    m, k = x.shape
+    return (x.is_cuda and 1 <= m <= SKINNY_MAX_M and w.shape[0] % 16 == 0
+            and k % (32 * SKINNY_WAVES) == 0 and x.stride(1) == 1 and w.is_contiguous())
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None,
+           out: torch.Tensor | None = None) -> torch.Tensor:
+    """y = x @ w.T (+ residual).  Decode-sized M runs the MFMA skinny GEMM; everything else
+    (prefill, CPU) runs F.linear (hipBLASLt on the GPU)."""
+    if skinny_ok(x, w):
+        if out is None:
+            out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
+        _native().skinny_gemm(out, x, w, residual, SKINNY_WAVES)
+        return out
+    y = torch.nn.functional.linear(x, w)
+    if residual is not None:
+        y = y + residual
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y

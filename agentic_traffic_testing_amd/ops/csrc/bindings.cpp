@@ -152,9 +152,33 @@ void sample(at::Tensor out, const at::Tensor& logits, const at::Tensor& temperat
            "sample");
 }
 
+void skinny_gemm(at::Tensor y, const at::Tensor& x, const at::Tensor& w,
+                 const c10::optional<at::Tensor>& residual, int64_t waves) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "skinny_gemm: 2-D operands");
+  TORCH_CHECK(x.stride(1) == 1 && y.stride(1) == 1 && w.is_contiguous(), "skinny_gemm: layout");
+  TORCH_CHECK(x.size(1) == w.size(1) && y.size(0) == x.size(0) && y.size(1) == w.size(0),
+              "skinny_gemm: shapes");
+  TORCH_CHECK(x.scalar_type() == w.scalar_type() && y.scalar_type() == x.scalar_type(),
+              "skinny_gemm: dtypes");
+  const void* r = nullptr;
+  int64_t rs = 0;
+  if (residual.has_value() && residual->defined()) {
+    TORCH_CHECK(residual->sizes() == y.sizes() && residual->stride(1) == 1, "skinny_gemm: residual");
+    r = residual->data_ptr();
+    rs = residual->stride(0);
+  }
+  const at::DeviceGuard g(x.device());
+  check_rc(atta_skinny_gemm(y.data_ptr(), x.data_ptr(), w.data_ptr(), r, x.size(0), w.size(0),
+                            w.size(1), x.stride(0), y.stride(0), rs, waves, dtype_code(x),
+                            cur_stream()),
+           "skinny_gemm");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(atta, m) {
+  m.def("skinny_gemm(Tensor(a!) y, Tensor x, Tensor w, Tensor? residual, int waves) -> ()");
   m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rms_norm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
@@ -182,4 +206,5 @@ TORCH_LIBRARY_IMPL(atta, CUDA, m) {
   m.impl("attention_prefill", &attention_prefill);
   m.impl("attention_decode", &attention_decode);
   m.impl("sample", &sample);
+  m.impl("skinny_gemm", &skinny_gemm);
 }

@@ -35,3 +35,7 @@ int atta_attention_decode(void* out, float* part_out, float* part_lse, const voi
 int atta_sample(int64_t* out, const void* logits, int rows, int vocab, int64_t stride,
                 int logits_is_fp32, const float* temperature, const int64_t* seeds,
                 const int64_t* steps, hipStream_t stream);
+
+int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual, int M, int N,
+                     int K, int64_t x_stride, int64_t y_stride, int64_t res_stride, int waves,
+                     int dtype, hipStream_t stream);

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Perf iteration: kernel tests (fast subset), GEMM microbench, bench, profile.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+OUT=gpurun_out; mkdir -p $OUT
+run() { local name=$1 t=$2; shift 2; echo "=== $name"; timeout -k 10 $t "$@" > $OUT/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; tail -${TAILN:-6} $OUT/$name.log; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo STOP; exit $rc; fi; }
+run pytest_gpu 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-}
+TAILN=30 run microbench 600 python scripts/gpu/microbench_gemm.py
+run bench 900 python bench.py --steps 2 --warmup 1 --verbose
+if [ "${PROFILE:-1}" = "1" ]; then
+  echo "=== profile"; bash scripts/gpu/profile_bench.sh
+fi

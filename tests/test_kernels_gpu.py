@@ -208,3 +208,20 @@ def test_sample_distribution():
     freq = torch.bincount(toks, minlength=V).float() / N
     p = torch.softmax(logits[0].cpu() / 0.8, -1)
     assert float((freq - p).abs().max()) < 0.03
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("m,n,k", [(1, 6144, 4096), (5, 4096, 4096), (12, 28672, 4096),
+                                   (16, 4096, 14336), (3, 128256, 4096), (24, 1024, 3584),
+                                   (64, 512, 8192)])
+def test_skinny_gemm(dtype, m, n, k):
+    torch.manual_seed(7)
+    x = torch.randn(m, k, dtype=dtype, device="cuda")
+    w = torch.randn(n, k, dtype=dtype, device="cuda") * 0.02
+    exp = (x.float() @ w.float().t())
+    got = ops.linear(x, w)
+    close(got, exp, 2e-2 * math.sqrt(k / 4096), 1e-2)
+    r = torch.randn(m, n, dtype=dtype, device="cuda")
+    got_r = ops.linear(x, w, residual=r)
+    exp_r = (exp.to(dtype).float() + r.float())
+    close(got_r, exp_r, 3e-2 * math.sqrt(k / 4096), 1e-2)
