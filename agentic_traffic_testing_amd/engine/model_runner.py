@@ -129,6 +129,22 @@ class ModelRunner:
                                     dtype=torch.float32, device=self.device)
         self.part_lse = torch.empty(self.max_seqs * nkv * self.max_parts * 16,
                                     dtype=torch.float32, device=self.device)
+        # fused decode-path workspace (q / attention / activation rows, sampler keys,
+        # split-K partials and arrival counters for the decode attention kernel)
+        H = self.mcfg.hidden_size
+        dt, dev = self.dtype, self.device
+        self.ws = {
+            "q": torch.empty(self.max_seqs, self.model.n_heads, 128, dtype=dt, device=dev),
+            "attn": torch.empty(self.max_seqs, self.model.n_heads, 128, dtype=dt, device=dev),
+            "act": torch.empty(self.max_seqs, self.model.inter, dtype=dt, device=dev),
+            "keys": torch.zeros(self.max_seqs, dtype=torch.int64, device=dev),
+            "tokens": torch.zeros(self.max_seqs, dtype=torch.int64, device=dev),
+            "counters": torch.zeros(self.max_seqs * nkv, dtype=torch.int32, device=dev),
+            "part_out": self.part_out, "part_lse": self.part_lse,
+            "max_parts": self.max_parts, "part_tokens": self.part_tokens,
+        }
+        del H
+        self.fused_decode = bool(cfg.fused_decode)
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_io: dict[int, dict] = {}
         self.graph_pool = None
@@ -212,6 +228,11 @@ class ModelRunner:
 
     def _forward_sample(self, v: dict, md: AttnMeta, num_parts: int, special_sampling=None):
         m = self.model
+        T = v["input_ids"].shape[0]
+        if (self.fused_decode and special_sampling is None and md.num_tiles == 0
+                and md.num_decode == T and m.decode_fusable(T)):
+            return m.forward_decode(v["input_ids"], md, self.k_layers, self.v_layers, self.ws,
+                                    v["temperature"], v["seeds"], v["steps"])
         hidden = m.forward(v["input_ids"], md, self.k_layers, self.v_layers, self.part_out,
                            self.part_lse, num_parts, self.part_tokens)
         last = hidden.index_select(0, v["logits_idx"])

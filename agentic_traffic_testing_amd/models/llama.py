@@ -109,7 +109,11 @@ class LlamaModel:
 
         H, D = cfg.hidden_size, cfg.head_dim
         self.embed = rnd((cfg.vocab_size, H), 1, 1.0)
-        self.norm = torch.ones(H, dtype=dt, device=dev)
+
+        def norm_w(tag):  # non-trivial norm weights so the folding is exercised
+            return (1.0 + rnd((H,), tag, 0.1).float()).to(dt)
+
+        self.norm = norm_w(3)
         lm = self.embed if cfg.tie_word_embeddings else rnd((cfg.vocab_size, H), 2)
         self.lm_head = self._shard_rows(lm, self.vocab_shard).contiguous()
         self.layers = []
@@ -122,10 +126,10 @@ class LlamaModel:
             wg = rnd((cfg.intermediate_size, H), base + 4)
             wu = rnd((cfg.intermediate_size, H), base + 5)
             wd = rnd((H, cfg.intermediate_size), base + 6) / math.sqrt(2 * cfg.num_layers) * 4
-            self.layers.append(self._make_layer(wq, wk, wv, wo, wg, wu, wd,
-                                                torch.ones(H, dtype=dt, device=dev),
-                                                torch.ones(H, dtype=dt, device=dev)))
+            self.layers.append(self._make_layer(wq, wk, wv, wo, wg, wu, wd, norm_w(base + 7),
+                                                norm_w(base + 8)))
             del wq, wk, wv, wo, wg, wu, wd
+        self._fold_final_norm()
         return self
 
     def _shard_rows(self, w: torch.Tensor, rows: int) -> torch.Tensor:
@@ -152,7 +156,23 @@ class LlamaModel:
         gu = torch.cat([self._shard_rows(wg, self.inter), self._shard_rows(wu, self.inter)],
                        0).contiguous()
         down = self._shard_cols(wd, self.inter).contiguous()
-        return LayerWeights(n_in.contiguous(), qkv, o, n_post.contiguous(), gu, down)
+        # Fold the RMSNorm weights into the following projections (x*w) W^T = x (W diag(w))^T:
+        # the decode kernels then only need the per-row rms, and the prefill path normalises
+        # with a unit weight.  Both paths see identical folded weights.
+        qkv = (qkv.float() * n_in.float()[None, :]).to(qkv.dtype).contiguous()
+        gu = (gu.float() * n_post.float()[None, :]).to(gu.dtype).contiguous()
+        ones = self._ones(n_in)
+        return LayerWeights(ones, qkv, o, ones, gu, down)
+
+    def _ones(self, like):
+        if getattr(self, "_ones_t", None) is None or self._ones_t.shape != like.shape:
+            self._ones_t = torch.ones_like(like)
+        return self._ones_t
+
+    def _fold_final_norm(self):
+        self.lm_head = (self.lm_head.float() * self.norm.float()[None, :]).to(
+            self.lm_head.dtype).contiguous()
+        self.norm = self._ones(self.norm)
 
     def load_safetensors(self, path: str):
         """Load HF Llama weights (model*.safetensors) and shard for this TP rank."""
@@ -187,6 +207,7 @@ class LlamaModel:
                 get(pre + "mlp.gate_proj.weight"), get(pre + "mlp.up_proj.weight"),
                 get(pre + "mlp.down_proj.weight"), get(pre + "input_layernorm.weight"),
                 get(pre + "post_attention_layernorm.weight")))
+        self._fold_final_norm()
         return self
 
     # ---------------------------------------------------------------------------------
@@ -236,6 +257,50 @@ class LlamaModel:
             a = ops.silu_and_mul(gu)
             h = self._all_reduce(ops.linear(a, L.down))
         return ops.fused_add_rms_norm(h, residual, self.norm, eps)
+
+    def decode_fusable(self, num_tokens: int) -> bool:
+        step = 32 * ops.SKINNY_WAVES
+        return (self.device.type == "cuda" and num_tokens <= ops.SKINNY_MAX_M
+                and self.cfg.hidden_size % step == 0 and self.inter % step == 0
+                and (self.n_heads * self.head_dim) % step == 0)
+
+    def forward_decode(self, input_ids: torch.Tensor, md: AttnMeta, k_caches, v_caches, ws: dict,
+                       temperature, seeds, steps) -> torch.Tensor:
+        """Fused decode step (every sequence has one query token); returns sampled ids.
+
+        Per layer: [RMSNorm+QKV+RoPE+KV-write] -> [paged attention, in-kernel split-K
+        combine] -> [o_proj + residual add] -> [RMSNorm+gate_up+SiLU*up] ->
+        [down_proj + residual add]; then [final RMSNorm + LM head + sampler].  5 kernels per
+        layer instead of ~10, no normalised activations or logits ever hit HBM."""
+        eps = self.cfg.rms_norm_eps
+        nq, nkv = self.n_heads, self.n_kv_heads
+        B = input_ids.shape[0]
+        residual = F.embedding(input_ids, self.embed)
+        q = ws["q"][:B]
+        attn = ws["attn"][:B]
+        act = ws["act"][:B]
+        for li, L in enumerate(self.layers):
+            ops.decode_qkv_rope(residual, L.qkv, eps, md.positions, md.slot_mapping, self.cos_sin,
+                                k_caches[li], v_caches[li], nq, nkv, q_out=q)
+            ops.attention_decode_v2(q, k_caches[li], v_caches[li], md.block_tables,
+                                    md.seq_kvlen, md.seq_qstart, self.scale, ws["part_out"],
+                                    ws["part_lse"], ws["counters"], ws["max_parts"],
+                                    ws["part_tokens"], out=attn, num_seqs=B)
+            if self.tp_size == 1:
+                ops.linear(attn.view(B, nq * self.head_dim), L.o, residual=residual)
+            else:
+                residual.add_(self._all_reduce(ops.linear(attn.view(B, nq * self.head_dim), L.o)))
+            ops.decode_gate_up_silu(residual, L.gate_up, eps, out=act)
+            if self.tp_size == 1:
+                ops.linear(act, L.down, residual=residual)
+            else:
+                residual.add_(self._all_reduce(ops.linear(act, L.down)))
+        if self.tp_size == 1:
+            return ops.decode_lm_head_sample(residual, self.lm_head, eps, temperature, seeds,
+                                             steps, ws["keys"], tokens=ws["tokens"][:B])
+        x = ops.rms_norm(residual, self.norm, eps)
+        logits = self.compute_logits(x)
+        return ops.sample(logits, temperature, seeds, steps, out=ws["tokens"][:B])
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
         logits = ops.linear(hidden, self.lm_head)

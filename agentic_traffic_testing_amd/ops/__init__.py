@@ -154,8 +154,8 @@ PREFILL_TILE_TOKENS = {1: 64, 2: 32, 4: 16, 8: 8}  # tokens per prefill workgrou
 
 # skinny-GEMM (decode) dispatch: rows <= SKINNY_MAX_M use the MFMA weight-streaming kernel,
 # larger M (prefill) goes to hipBLASLt through F.linear.
-SKINNY_MAX_M = int(os.environ.get("ATTA_SKINNY_MAX_M", "64"))
-SKINNY_WAVES = int(os.environ.get("ATTA_SKINNY_WAVES", "4"))
+SKINNY_MAX_M = int(os.environ.get("ATTA_SKINNY_MAX_M", "32"))
+SKINNY_WAVES = int(os.environ.get("ATTA_SKINNY_WAVES", "8"))
 
 
 def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -166,17 +166,82 @@ def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 
 def linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None,
            out: torch.Tensor | None = None) -> torch.Tensor:
-    """y = x @ w.T (+ residual).  Decode-sized M runs the MFMA skinny GEMM; everything else
-    (prefill, CPU) runs F.linear (hipBLASLt on the GPU)."""
+    """y = x @ w.T.  With ``residual`` the product is added to ``residual`` IN PLACE and
+    ``residual`` is returned (residual-stream update).  Decode-sized M runs the MFMA skinny
+    GEMM; everything else (prefill, CPU) runs F.linear (hipBLASLt on the GPU)."""
     if skinny_ok(x, w):
+        if residual is not None:
+            _native().skinny_gemm(residual, x, w, residual, SKINNY_WAVES)
+            return residual
         if out is None:
             out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
-        _native().skinny_gemm(out, x, w, residual, SKINNY_WAVES)
+        _native().skinny_gemm(out, x, w, None, SKINNY_WAVES)
         return out
     y = torch.nn.functional.linear(x, w)
     if residual is not None:
-        y = y + residual
+        residual.copy_((y.float() + residual.float()).to(residual.dtype))
+        return residual
     if out is not None:
         out.copy_(y)
         return out
     return y
+
+
+# ---- fused decode-step ops (norm weight folded into W on the host) -----------------------
+def decode_qkv_rope(x, w, eps, positions, slots, cos_sin, k_cache, v_cache, n_q_heads,
+                    n_kv_heads, q_out=None):
+    """RMSNorm(x) -> QKV GEMM -> RoPE -> q out + paged K/V write, one kernel on the GPU."""
+    if q_out is None:
+        q_out = torch.empty(x.shape[0], n_q_heads, 128, dtype=x.dtype, device=x.device)
+    if not x.is_cuda:
+        n = ref.rms_norm(x, torch.ones(x.shape[1], dtype=x.dtype), eps)
+        q = ref.rope_cache(torch.nn.functional.linear(n, w), positions, slots, cos_sin, k_cache,
+                           v_cache, n_q_heads, n_kv_heads, 128)
+        q_out.copy_(q)
+        return q_out
+    _native().fused_qkv_rope(q_out, k_cache, v_cache, x, w, positions, slots, cos_sin,
+                             n_q_heads, n_kv_heads, eps, SKINNY_WAVES)
+    return q_out
+
+
+def decode_gate_up_silu(x, w, eps, out=None):
+    """RMSNorm(x) -> gate_up GEMM -> SiLU(gate) * up, one kernel on the GPU."""
+    inter = w.shape[0] // 2
+    if out is None:
+        out = torch.empty(x.shape[0], inter, dtype=x.dtype, device=x.device)
+    if not x.is_cuda:
+        n = ref.rms_norm(x, torch.ones(x.shape[1], dtype=x.dtype), eps)
+        out.copy_(ref.silu_and_mul(torch.nn.functional.linear(n, w)))
+        return out
+    _native().fused_gate_up_silu(out, x, w, eps, SKINNY_WAVES)
+    return out
+
+
+def decode_lm_head_sample(x, w, eps, temperature, seeds, steps, keys, tokens=None,
+                          finalize=True):
+    """Final RMSNorm -> LM head -> greedy / Gumbel-max sample without materialising logits.
+    ``keys`` (int64 [M], zero-initialised once) holds packed (value, index) maxima."""
+    if tokens is None:
+        tokens = torch.empty(x.shape[0], dtype=torch.long, device=x.device)
+    if not x.is_cuda:
+        n = ref.rms_norm(x, torch.ones(x.shape[1], dtype=x.dtype), eps)
+        tokens.copy_(ref.sample(torch.nn.functional.linear(n, w), temperature, seeds, steps))
+        return tokens
+    _native().fused_lm_head_sample(tokens, keys, x, w, eps, temperature, seeds, steps, finalize,
+                                   SKINNY_WAVES)
+    return tokens
+
+
+def attention_decode_v2(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, scale,
+                        part_out, part_lse, counters, max_parts, part_tokens, out=None,
+                        num_seqs: int = -1):
+    """Decode attention with in-kernel split-K combine (one launch)."""
+    if not q.is_cuda:
+        n = seq_kvlen.shape[0] if num_seqs < 0 else num_seqs
+        return ref.paged_attention(q, k_cache, v_cache, block_tables[:n], seq_kvlen[:n],
+                                   seq_qstart[:n + 1], scale, out=out)
+    out = torch.empty_like(q) if out is None else out
+    _native().attention_decode_v2(out, part_out, part_lse, counters, q, k_cache, v_cache,
+                                  block_tables, seq_kvlen, seq_qstart, num_seqs, max_parts,
+                                  part_tokens, q.shape[1], k_cache.shape[1], scale)
+    return out

@@ -175,9 +175,130 @@ void skinny_gemm(at::Tensor y, const at::Tensor& x, const at::Tensor& w,
            "skinny_gemm");
 }
 
+void check_skinny(const at::Tensor& x, const at::Tensor& w, const char* what) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.is_contiguous(), what,
+              ": layout");
+  TORCH_CHECK(x.size(1) == w.size(1) && x.scalar_type() == w.scalar_type(), what, ": shapes");
+}
+
+void fused_qkv_rope(at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache, const at::Tensor& x,
+                    const at::Tensor& w, const at::Tensor& positions, const at::Tensor& slots,
+                    const at::Tensor& cos_sin, int64_t n_q_heads, int64_t n_kv_heads, double eps,
+                    int64_t waves) {
+  check_skinny(x, w, "fused_qkv_rope");
+  TORCH_CHECK(w.size(0) == (n_q_heads + 2 * n_kv_heads) * 128, "fused_qkv_rope: w rows");
+  TORCH_CHECK(positions.scalar_type() == at::kInt && slots.scalar_type() == at::kInt,
+              "fused_qkv_rope: int32 positions/slots");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(1) == 128, "fused_qkv_rope: cos_sin");
+  TORCH_CHECK(q_out.stride(-1) == 1, "fused_qkv_rope: q_out layout");
+  TORCH_CHECK(k_cache.size(1) == n_kv_heads && k_cache.size(3) == 128, "fused_qkv_rope: k_cache");
+  const at::DeviceGuard g(x.device());
+  check_rc(atta_fused_qkv_rope(q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                               x.data_ptr(), w.data_ptr(), positions.data_ptr<int>(),
+                               slots.data_ptr<int>(), cos_sin.data_ptr<float>(), x.size(0),
+                               x.size(1), x.stride(0), q_out.stride(0), n_q_heads, n_kv_heads,
+                               k_cache.size(2), static_cast<float>(eps), waves, dtype_code(x),
+                               cur_stream()),
+           "fused_qkv_rope");
+}
+
+void fused_gate_up_silu(at::Tensor out, const at::Tensor& x, const at::Tensor& w, double eps,
+                        int64_t waves) {
+  check_skinny(x, w, "fused_gate_up_silu");
+  TORCH_CHECK(w.size(0) == 2 * out.size(1) && out.size(0) == x.size(0) && out.stride(1) == 1,
+              "fused_gate_up_silu: out");
+  const at::DeviceGuard g(x.device());
+  check_rc(atta_fused_gate_up_silu(out.data_ptr(), x.data_ptr(), w.data_ptr(), x.size(0),
+                                   x.size(1), out.size(1), x.stride(0), out.stride(0),
+                                   static_cast<float>(eps), waves, dtype_code(x), cur_stream()),
+           "fused_gate_up_silu");
+}
+
+void fused_lm_head_sample(at::Tensor tokens, at::Tensor keys, const at::Tensor& x,
+                          const at::Tensor& w, double eps, const at::Tensor& temperature,
+                          const at::Tensor& seeds, const at::Tensor& steps, bool finalize,
+                          int64_t waves) {
+  check_skinny(x, w, "fused_lm_head_sample");
+  TORCH_CHECK(tokens.scalar_type() == at::kLong && keys.scalar_type() == at::kLong &&
+                  seeds.scalar_type() == at::kLong && steps.scalar_type() == at::kLong &&
+                  temperature.scalar_type() == at::kFloat,
+              "fused_lm_head_sample: dtypes");
+  TORCH_CHECK(keys.numel() >= x.size(0) && tokens.numel() >= x.size(0), "fused_lm_head_sample: sizes");
+  const at::DeviceGuard g(x.device());
+  check_rc(atta_fused_lm_head_sample(
+               tokens.data_ptr<int64_t>(),
+               reinterpret_cast<unsigned long long*>(keys.data_ptr<int64_t>()), x.data_ptr(),
+               w.data_ptr(), x.size(0), w.size(0), x.size(1), x.stride(0), static_cast<float>(eps),
+               temperature.data_ptr<float>(), seeds.data_ptr<int64_t>(), steps.data_ptr<int64_t>(),
+               finalize ? 1 : 0, waves, dtype_code(x), cur_stream()),
+           "fused_lm_head_sample");
+}
+
+void sample_finalize(at::Tensor tokens, at::Tensor keys) {
+  check_dev(keys, "keys");
+  const at::DeviceGuard g(keys.device());
+  check_rc(atta_sample_finalize(tokens.data_ptr<int64_t>(),
+                                reinterpret_cast<unsigned long long*>(keys.data_ptr<int64_t>()),
+                                keys.numel(), cur_stream()),
+           "sample_finalize");
+}
+
+void attention_decode_v2(at::Tensor out, at::Tensor part_out, at::Tensor part_lse,
+                         at::Tensor counters, const at::Tensor& q, const at::Tensor& k_cache,
+                         const at::Tensor& v_cache, const at::Tensor& block_tables,
+                         const at::Tensor& seq_kvlen, const at::Tensor& seq_qstart,
+                         int64_t num_seqs, int64_t max_parts, int64_t part_tokens,
+                         int64_t n_q_heads, int64_t n_kv_heads, double scale) {
+  check_dev(q, "q");
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && seq_kvlen.scalar_type() == at::kInt &&
+                  seq_qstart.scalar_type() == at::kInt && counters.scalar_type() == at::kInt,
+              "attention_decode_v2: int32 metadata");
+  if (num_seqs < 0) num_seqs = seq_kvlen.size(0);
+  TORCH_CHECK(num_seqs <= seq_kvlen.size(0), "attention_decode_v2: num_seqs");
+  TORCH_CHECK(part_out.numel() >= num_seqs * n_kv_heads * max_parts * 16 * 128 &&
+                  part_lse.numel() >= num_seqs * n_kv_heads * max_parts * 16 &&
+                  counters.numel() >= num_seqs * n_kv_heads,
+              "attention_decode_v2: workspace too small");
+  const at::DeviceGuard g(q.device());
+  check_rc(atta_attention_decode_v2(
+               out.data_ptr(), part_out.data_ptr<float>(), part_lse.data_ptr<float>(),
+               counters.data_ptr<int>(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+               block_tables.data_ptr<int>(), seq_kvlen.data_ptr<int>(), seq_qstart.data_ptr<int>(),
+               num_seqs, max_parts, part_tokens, n_q_heads, n_kv_heads, k_cache.size(3),
+               k_cache.size(2), block_tables.stride(0), q.stride(0), out.stride(0),
+               static_cast<float>(scale), dtype_code(q), cur_stream()),
+           "attention_decode_v2");
+}
+
+void skinny_variant(at::Tensor y, const at::Tensor& x, const at::Tensor& w, int64_t variant) {
+  check_skinny(x, w, "skinny_variant");
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.scalar_type() == at::kBFloat16,
+              "skinny_variant: contiguous bf16");
+  const at::DeviceGuard g(x.device());
+  check_rc(atta_skinny_variant(y.data_ptr(), x.data_ptr(), w.data_ptr(), x.size(0), w.size(0),
+                               w.size(1), static_cast<int>(variant), cur_stream()),
+           "skinny_variant");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(atta, m) {
+  m.def("skinny_variant(Tensor(a!) y, Tensor x, Tensor w, int variant) -> ()");
+  m.def(
+      "attention_decode_v2(Tensor(a!) out, Tensor(b!) part_out, Tensor(c!) part_lse, "
+      "Tensor(d!) counters, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
+      "Tensor seq_kvlen, Tensor seq_qstart, int num_seqs, int max_parts, int part_tokens, "
+      "int n_q_heads, int n_kv_heads, float scale) -> ()");
+  m.def(
+      "fused_qkv_rope(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor x, "
+      "Tensor w, Tensor positions, Tensor slots, Tensor cos_sin, int n_q_heads, int n_kv_heads, "
+      "float eps, int waves) -> ()");
+  m.def("fused_gate_up_silu(Tensor(a!) out, Tensor x, Tensor w, float eps, int waves) -> ()");
+  m.def(
+      "fused_lm_head_sample(Tensor(a!) tokens, Tensor(b!) keys, Tensor x, Tensor w, float eps, "
+      "Tensor temperature, Tensor seeds, Tensor steps, bool finalize, int waves) -> ()");
+  m.def("sample_finalize(Tensor(a!) tokens, Tensor(b!) keys) -> ()");
   m.def("skinny_gemm(Tensor(a!) y, Tensor x, Tensor w, Tensor? residual, int waves) -> ()");
   m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rms_norm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");
@@ -207,4 +328,10 @@ TORCH_LIBRARY_IMPL(atta, CUDA, m) {
   m.impl("attention_decode", &attention_decode);
   m.impl("sample", &sample);
   m.impl("skinny_gemm", &skinny_gemm);
+  m.impl("fused_qkv_rope", &fused_qkv_rope);
+  m.impl("fused_gate_up_silu", &fused_gate_up_silu);
+  m.impl("fused_lm_head_sample", &fused_lm_head_sample);
+  m.impl("sample_finalize", &sample_finalize);
+  m.impl("attention_decode_v2", &attention_decode_v2);
+  m.impl("skinny_variant", &skinny_variant);
 }

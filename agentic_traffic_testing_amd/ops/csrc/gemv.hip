@@ -1,21 +1,35 @@
-// Skinny (decode) GEMM on MFMA: y[M, N] = x[M, K] . W[N, K]^T  (+ residual), M <= 64.
+// Skinny (decode) GEMM on MFMA with fused prologue/epilogues.
+//
+//   acc[M, 16-col tile] = x[M, K] . W[rows(tile), K]^T          (M <= 32, W streamed once)
 //
 // Decode steps of the 8B model stream ~15 GB of weights per token while M (= sequences in
-// the batch) is 1..16, so the layer GEMMs are pure HBM streams.  Design (guide: "GEMV /
-// M <= 16 decode weights: load straight to VGPRs, deep unroll, late vmcnt"):
-//   * one workgroup owns 16 output features (16 weight rows); its WAVES waves split K, each
-//     streams its K slice of the 16 rows with 16-byte loads (UNROLL loads in flight/wave);
-//   * the 16 rows x 32 k chunk a wave loads is exactly the B operand of
-//     mfma_f32_16x16x32_bf16 (lane l: row n0 + (l&15), k = 8(l>>4)..+8), the x chunk is the A
-//     operand (lane l: x row l&15) - x is tiny and L1/L2 resident, rows >= M are zeros;
-//     MT 16-row tiles of x reuse each weight fragment (M up to 16*MT);
-//   * partial 16x16 tiles of the waves are summed through LDS; the epilogue optionally
-//     adds a residual row block (o_proj / down_proj -> residual stream).
-// grid = N / 16 workgroups (256 for N = 4096, 1792 for the gate_up projection).
+// the batch) is 1..16, so the layer GEMMs are pure HBM streams (guide: "GEMV / M <= 16
+// decode weights: load straight to VGPRs, deep unroll, late vmcnt").  Structure:
+//   * a workgroup owns one 16-column output tile; WAVES waves split K; each wave streams
+//     its K slice of the tile's 16 weight rows with 16-byte loads, two register stages of
+//     UNROLL loads each (software pipelined: the next stage is in flight while the current
+//     one feeds the MFMAs);
+//   * the 16 rows x 32 k chunk is the B operand of mfma_f32_16x16x32_bf16 (lane l: weight
+//     row rows(tile, l&15), k = 8(l>>4)..+8); x rows are the A operand (lane l: row l&15,
+//     L1/L2 resident; rows >= M are zeros);
+//   * `rows(tile, c)` is an epilogue-defined row map, so the epilogue can see partner
+//     columns without any weight permutation: RoPE pairs (d, d+64) and SwiGLU pairs
+//     (gate_j, up_j) land in the same tile;
+//   * RMSNorm fusion: with the norm weight folded into W on the host, the kernel only needs
+//     sum(x^2) per row, accumulated from the x fragments it already loads for the MFMAs;
+//     the epilogue scales by rsqrt(mean + eps);
+//   * wave partials + row sums are reduced through LDS; epilogues:
+//       PLAIN   y = acc                      RESADD  r += acc (residual stream, in place)
+//       QKVROPE q/k rotated (RoPE) -> q buffer / paged K cache, v -> transposed V cache
+//       SILU    out[:, j] = silu(gate_j) * up_j
+//       SAMPLE  logits -> greedy / Gumbel-max key -> atomicMax per row (sampler fused
+//               into the LM head; `sample_finalize` turns keys into token ids)
 #include "common.h"
 #include "kernels.h"
 
 namespace atta {
+
+enum Epi { EPI_PLAIN = 0, EPI_RESADD = 1, EPI_QKVROPE = 2, EPI_SILU = 3, EPI_SAMPLE = 4 };
 
 template <typename T>
 struct MfmaK32;
@@ -25,6 +39,15 @@ struct MfmaK32<__bf16> {
   __device__ static __forceinline__ f32x4 mma(frag8 a, frag8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
   }
+  __device__ static __forceinline__ float sq8(frag8 a) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = static_cast<float>(a[j]);
+      s += v * v;
+    }
+    return s;
+  }
 };
 template <>
 struct MfmaK32<_Float16> {
@@ -32,42 +55,110 @@ struct MfmaK32<_Float16> {
   __device__ static __forceinline__ f32x4 mma(frag8 a, frag8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
   }
+  __device__ static __forceinline__ float sq8(frag8 a) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = static_cast<float>(a[j]);
+      s += v * v;
+    }
+    return s;
+  }
 };
 
-template <typename T, int WAVES, int UNROLL, int MT>
-__global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
-    uint16_t* __restrict__ y, const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
-    const uint16_t* __restrict__ res, int M, int N, int K, int64_t x_stride, int64_t y_stride,
-    int64_t res_stride) {
-  using frag8 = typename MfmaK32<T>::frag8;
-  __shared__ float red[WAVES][MT][16][17];
+struct SkinnyParams {
+  const uint16_t* x;
+  const uint16_t* w;
+  uint16_t* y;  // PLAIN / RESADD (in place) / SILU output / QKVROPE q output
+  int64_t x_stride, y_stride;
+  int M, N, K;
+  float eps;  // > 0: fused RMSNorm (norm weight folded into W)
+  // QKVROPE
+  uint16_t* k_cache;
+  uint16_t* v_cache;
+  const int* positions;
+  const int* slots;
+  const float* cos_sin;
+  int n_q_heads, n_kv_heads, bs_shift;
+  // SILU
+  int inter;
+  // SAMPLE
+  unsigned long long* keys;
+  const float* temperature;
+  const int64_t* seeds;
+  const int64_t* steps;
+};
+
+__device__ __forceinline__ unsigned ordered_bits(float f) {
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ float gumbel_noise(uint64_t seed, uint64_t step, uint32_t idx) {
+  const uint64_t h = mix64(seed ^ mix64(step * 0x100000001B3ull + idx));
+  const float u = (static_cast<float>(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
+  return -__logf(-__logf(u));
+}
+
+template <int EPI>
+__device__ __forceinline__ int tile_row(int tile, int c, const SkinnyParams& p) {
+  if constexpr (EPI == EPI_QKVROPE) {
+    // head-dim 128: tile = head * 8 + j covers dims {8j..8j+7} and {64+8j..64+8j+7}
+    const int head = tile >> 3, j = tile & 7;
+    return head * 128 + j * 8 + (c & 7) + ((c & 8) ? 64 : 0);
+  } else if constexpr (EPI == EPI_SILU) {
+    return (c < 8) ? (tile * 8 + c) : (p.inter + tile * 8 + c - 8);
+  } else {
+    return tile * 16 + c;
+  }
+}
+
+template <typename T, int WAVES, int UNROLL, int MT, int EPI, bool NTL = true>
+__global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
+  using MF = MfmaK32<T>;
+  using frag8 = typename MF::frag8;
+  constexpr int R = MT * 16;
+  __shared__ float red[WAVES][R][17];
+  __shared__ float ssq[WAVES][R];
+  __shared__ float inv_rms[R];
+
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int col = lane & 15;
   const int grp = lane >> 4;
-  const int n0 = blockIdx.x * 16;
-  const int kw = K / WAVES;  // K % (32 * WAVES) == 0 checked on the host
+  const int tile = blockIdx.x;
+  const int kw = p.K / WAVES;
   const int kbeg = wid * kw;
-  const uint16_t* wp = w + static_cast<int64_t>(n0 + col) * K + kbeg + 8 * grp;
+  const int wrow = tile_row<EPI>(tile, col, p);
+  const uint16_t* wp = p.w + static_cast<int64_t>(wrow) * p.K + kbeg + 8 * grp;
   const uint16_t* xp[MT];
   bool xv[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) {
     const int m = t * 16 + col;
-    xv[t] = m < M;
-    xp[t] = x + static_cast<int64_t>(xv[t] ? m : 0) * x_stride + kbeg + 8 * grp;
+    xv[t] = m < p.M;
+    xp[t] = p.x + static_cast<int64_t>(xv[t] ? m : 0) * p.x_stride + kbeg + 8 * grp;
   }
   f32x4 acc[MT];
+  float ss[MT];
 #pragma unroll
-  for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < MT; ++t) {
+    acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    ss[t] = 0.f;
+  }
+  const bool norm = p.eps > 0.f;
 
-  int k = 0;
   constexpr int STEP = 32 * UNROLL;
-  for (; k + STEP <= kw; k += STEP) {
-    frag8 wf[UNROLL];
+  const int nsteps = kw / STEP;
+  auto load_w = [&](frag8 (&f)[UNROLL], int k) {
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u)
-      wf[u] = __builtin_nontemporal_load(reinterpret_cast<const frag8*>(wp + k + 32 * u));
+      if constexpr (NTL)
+        f[u] = __builtin_nontemporal_load(reinterpret_cast<const frag8*>(wp + k + 32 * u));
+      else
+        f[u] = *reinterpret_cast<const frag8*>(wp + k + 32 * u);
+  };
+  auto compute = [&](const frag8 (&f)[UNROLL], int k) {
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       frag8 xf[UNROLL];
@@ -75,58 +166,174 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
       for (int u = 0; u < UNROLL; ++u)
         xf[u] = xv[t] ? *reinterpret_cast<const frag8*>(xp[t] + k + 32 * u) : frag8{};
 #pragma unroll
-      for (int u = 0; u < UNROLL; ++u) acc[t] = MfmaK32<T>::mma(xf[u], wf[u], acc[t]);
+      for (int u = 0; u < UNROLL; ++u) {
+        acc[t] = MF::mma(xf[u], f[u], acc[t]);
+        if (norm) ss[t] += MF::sq8(xf[u]);
+      }
     }
+  };
+  if (nsteps > 0) {
+    frag8 wa[UNROLL], wb[UNROLL];
+    load_w(wa, 0);
+    int s = 0;
+    for (; s + 2 <= nsteps; s += 2) {
+      load_w(wb, (s + 1) * STEP);
+      compute(wa, s * STEP);
+      if (s + 2 < nsteps) load_w(wa, (s + 2) * STEP);
+      compute(wb, (s + 1) * STEP);
+    }
+    if (s < nsteps) compute(wa, s * STEP);
   }
-  for (; k < kw; k += 32) {
-    frag8 wf = __builtin_nontemporal_load(reinterpret_cast<const frag8*>(wp + k));
+  for (int k = nsteps * STEP; k < kw; k += 32) {  // tail (K not a multiple of the stage)
+    const frag8 wf = __builtin_nontemporal_load(reinterpret_cast<const frag8*>(wp + k));
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
-      frag8 xf = xv[t] ? *reinterpret_cast<const frag8*>(xp[t] + k) : frag8{};
-      acc[t] = MfmaK32<T>::mma(xf, wf, acc[t]);
+      const frag8 xf = xv[t] ? *reinterpret_cast<const frag8*>(xp[t] + k) : frag8{};
+      acc[t] = MF::mma(xf, wf, acc[t]);
+      if (norm) ss[t] += MF::sq8(xf);
     }
   }
 
-  // C layout: row m = 4*grp + i, col n = lane & 15
+  // ---- cross-wave reduction ------------------------------------------------------------
 #pragma unroll
-  for (int t = 0; t < MT; ++t)
+  for (int t = 0; t < MT; ++t) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) red[wid][t][4 * grp + i][col] = acc[t][i];
+    for (int i = 0; i < 4; ++i) red[wid][t * 16 + 4 * grp + i][col] = acc[t][i];
+    if (norm) {
+      float v = ss[t];
+      v += __shfl_xor(v, 16, kWave);
+      v += __shfl_xor(v, 32, kWave);
+      if (grp == 0) ssq[wid][t * 16 + col] = v;
+    }
+  }
   __syncthreads();
-  for (int e = threadIdx.x; e < MT * 256; e += WAVES * 64) {
-    const int t = e >> 8;
-    const int m = (e >> 4) & 15;
-    const int n = e & 15;
-    const int row = t * 16 + m;
-    if (row >= M) continue;
+  if (norm && threadIdx.x < R) {
     float s = 0.f;
 #pragma unroll
-    for (int q = 0; q < WAVES; ++q) s += red[q][t][m][n];
-    if (res != nullptr) {
-      // round the GEMM result first (matches F.linear followed by a bf16 add)
-      s = to_f32<T>(from_f32<T>(s)) + to_f32<T>(res[static_cast<int64_t>(row) * res_stride + n0 + n]);
+    for (int q = 0; q < WAVES; ++q) s += ssq[q][threadIdx.x];
+    inv_rms[threadIdx.x] = rsqrtf(s / static_cast<float>(p.K) + p.eps);
+  }
+  // sum wave partials into red[0]
+  for (int e = threadIdx.x; e < R * 16; e += WAVES * 64) {
+    const int m = e >> 4, n = e & 15;
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < WAVES; ++q) s += red[q][m][n];
+    red[0][m][n] = s;
+  }
+  __syncthreads();
+
+  // ---- epilogues -----------------------------------------------------------------------
+  if constexpr (EPI == EPI_PLAIN || EPI == EPI_RESADD) {
+    for (int e = threadIdx.x; e < R * 16; e += WAVES * 64) {
+      const int m = e >> 4, n = e & 15;
+      if (m >= p.M) continue;
+      float v = red[0][m][n];
+      if (norm) v *= inv_rms[m];
+      uint16_t* dst = p.y + static_cast<int64_t>(m) * p.y_stride + tile * 16 + n;
+      if constexpr (EPI == EPI_RESADD) v = to_f32<T>(from_f32<T>(v)) + to_f32<T>(*dst);
+      *dst = from_f32<T>(v);
     }
-    y[static_cast<int64_t>(row) * y_stride + n0 + n] = from_f32<T>(s);
+  } else if constexpr (EPI == EPI_SILU) {
+    for (int e = threadIdx.x; e < R * 8; e += WAVES * 64) {
+      const int m = e >> 3, j = e & 7;
+      if (m >= p.M) continue;
+      const float sc = norm ? inv_rms[m] : 1.f;
+      const float g = to_f32<T>(from_f32<T>(red[0][m][j] * sc));
+      const float u = to_f32<T>(from_f32<T>(red[0][m][j + 8] * sc));
+      const float si = to_f32<T>(from_f32<T>(g / (1.f + __expf(-g))));
+      p.y[static_cast<int64_t>(m) * p.y_stride + tile * 8 + j] = from_f32<T>(si * u);
+    }
+  } else if constexpr (EPI == EPI_QKVROPE) {
+    const int head = tile >> 3, jb = (tile & 7) * 8;
+    const int nq = p.n_q_heads, nkv = p.n_kv_heads;
+    const int BS = 1 << p.bs_shift;
+    for (int e = threadIdx.x; e < R * 8; e += WAVES * 64) {
+      const int m = e >> 3, c = e & 7;
+      if (m >= p.M) continue;
+      const float sc = norm ? inv_rms[m] : 1.f;
+      // GEMM output rounded to T first (matches the unfused F.linear -> rope path)
+      const float x1 = to_f32<T>(from_f32<T>(red[0][m][c] * sc));
+      const float x2 = to_f32<T>(from_f32<T>(red[0][m][c + 8] * sc));
+      const int d = jb + c;  // < 64
+      const int slot = p.slots[m];
+      if (head < nq + nkv) {
+        const float* cs = p.cos_sin + static_cast<int64_t>(p.positions[m]) * 128;
+        const float co = cs[d], si = cs[64 + d];
+        const uint16_t o1 = from_f32<T>(x1 * co - x2 * si);
+        const uint16_t o2 = from_f32<T>(x2 * co + x1 * si);
+        if (head < nq) {
+          uint16_t* q = p.y + static_cast<int64_t>(m) * p.y_stride + head * 128;
+          q[d] = o1;
+          q[d + 64] = o2;
+        } else if (slot >= 0) {
+          const int hk = head - nq;
+          uint16_t* kc = p.k_cache + ((static_cast<int64_t>(slot >> p.bs_shift) * nkv + hk) * BS +
+                                      (slot & (BS - 1))) * 128;
+          kc[d] = o1;
+          kc[d + 64] = o2;
+        }
+      } else if (slot >= 0) {
+        const int hk = head - nq - nkv;
+        uint16_t* vc = p.v_cache + (static_cast<int64_t>(slot >> p.bs_shift) * nkv + hk) * 128 * BS +
+                       (slot & (BS - 1));
+        vc[static_cast<int64_t>(d) * BS] = from_f32<T>(x1);
+        vc[static_cast<int64_t>(d + 64) * BS] = from_f32<T>(x2);
+      }
+    }
+  } else if constexpr (EPI == EPI_SAMPLE) {
+    // one row per thread group of 16 columns: thread e handles (m, n) and reduces over n
+    for (int e = threadIdx.x; e < R * 16; e += WAVES * 64) {
+      const int m = e >> 4, n = e & 15;
+      unsigned long long key = 0ull;
+      if (m < p.M) {
+        const float sc = norm ? inv_rms[m] : 1.f;
+        float v = to_f32<T>(from_f32<T>(red[0][m][n] * sc));  // bf16 logits, as F.linear
+        const float t = p.temperature[m];
+        const int idx = tile * 16 + n;
+        if (t > 1e-5f)
+          v = v / t + gumbel_noise(static_cast<uint64_t>(p.seeds[m]),
+                                   static_cast<uint64_t>(p.steps[m]), static_cast<uint32_t>(idx));
+        key = (static_cast<unsigned long long>(ordered_bits(v)) << 32) |
+              static_cast<unsigned long long>(0xFFFFFFFFu - static_cast<unsigned>(idx));
+      }
+      // max over the 16 columns of this row: lanes e..e+15 are contiguous in a wave
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const unsigned long long other = __shfl_xor(key, o, kWave);
+        key = other > key ? other : key;
+      }
+      if (n == 0 && m < p.M) atomicMax(p.keys + m, key);
+    }
   }
 }
 
-template <typename T, int WAVES, int UNROLL>
-static void launch_skinny(int mt, dim3 grid, hipStream_t st, uint16_t* y, const uint16_t* x,
-                          const uint16_t* w, const uint16_t* res, int M, int N, int K,
-                          int64_t xs, int64_t ys, int64_t rs) {
-  switch (mt) {
-    case 1:
-      skinny_gemm_kernel<T, WAVES, UNROLL, 1><<<grid, WAVES * 64, 0, st>>>(y, x, w, res, M, N, K,
-                                                                          xs, ys, rs);
-      break;
-    case 2:
-      skinny_gemm_kernel<T, WAVES, UNROLL, 2><<<grid, WAVES * 64, 0, st>>>(y, x, w, res, M, N, K,
-                                                                          xs, ys, rs);
-      break;
-    default:
-      skinny_gemm_kernel<T, WAVES, UNROLL, 4><<<grid, WAVES * 64, 0, st>>>(y, x, w, res, M, N, K,
-                                                                          xs, ys, rs);
-      break;
+template <int WAVES, int UNROLL, int MT, int EPI>
+static void launch_t(int dtype, dim3 grid, hipStream_t st, const SkinnyParams& p) {
+  if (dtype == 0)
+    skinny_kernel<__bf16, WAVES, UNROLL, MT, EPI><<<grid, WAVES * 64, 0, st>>>(p);
+  else
+    skinny_kernel<_Float16, WAVES, UNROLL, MT, EPI><<<grid, WAVES * 64, 0, st>>>(p);
+}
+
+template <int EPI>
+static void launch_epi(int dtype, int mt, int waves, dim3 grid, hipStream_t st,
+                       const SkinnyParams& p) {
+  if (waves == 8) {
+    if (mt == 1) launch_t<8, 4, 1, EPI>(dtype, grid, st, p);
+    else launch_t<8, 4, 2, EPI>(dtype, grid, st, p);
+  } else {
+    if (mt == 1) launch_t<4, 4, 1, EPI>(dtype, grid, st, p);
+    else launch_t<4, 4, 2, EPI>(dtype, grid, st, p);
+  }
+}
+
+__global__ void sample_finalize_kernel(int64_t* out, unsigned long long* keys, int M) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m < M) {
+    const unsigned long long k = keys[m];
+    out[m] = static_cast<int64_t>(0xFFFFFFFFu - static_cast<unsigned>(k & 0xFFFFFFFFull));
+    keys[m] = 0ull;  // re-arm for the next launch (keys start zeroed at allocation)
   }
 }
 
@@ -134,32 +341,151 @@ static void launch_skinny(int mt, dim3 grid, hipStream_t st, uint16_t* y, const 
 
 using namespace atta;
 
+static int skinny_checks(int M, int K, int waves) {
+  if (M < 1 || M > 32) return -1;
+  if (K % (32 * waves) != 0) return -1;
+  return 0;
+}
+
 int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual, int M, int N,
                      int K, int64_t x_stride, int64_t y_stride, int64_t res_stride, int waves,
                      int dtype, hipStream_t stream) {
-  if (M < 1 || M > 64 || N % 16 != 0) return -1;
-  if (waves != 4 && waves != 8) waves = 4;
-  if (K % (32 * waves) != 0) return -1;
-  const int mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  if (waves != 4 && waves != 8) waves = 8;
+  if (skinny_checks(M, K, waves) || N % 16 != 0) return -1;
+  SkinnyParams p{};
+  p.x = static_cast<const uint16_t*>(x);
+  p.w = static_cast<const uint16_t*>(w);
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.x_stride = x_stride;
+  p.eps = 0.f;
+  const int mt = M <= 16 ? 1 : 2;
   dim3 grid(N / 16);
-  auto yo = static_cast<uint16_t*>(y);
-  auto xi = static_cast<const uint16_t*>(x);
-  auto wi = static_cast<const uint16_t*>(w);
-  auto ri = static_cast<const uint16_t*>(residual);
-  if (dtype == 0) {
-    if (waves == 8)
-      launch_skinny<__bf16, 8, 8>(mt, grid, stream, yo, xi, wi, ri, M, N, K, x_stride, y_stride,
-                                  res_stride);
-    else
-      launch_skinny<__bf16, 4, 8>(mt, grid, stream, yo, xi, wi, ri, M, N, K, x_stride, y_stride,
-                                  res_stride);
+  if (residual != nullptr) {
+    // y := residual + x W^T, computed in place on the residual buffer when y == residual;
+    // otherwise copy semantics are not supported (callers pass y == residual).
+    if (residual != y) return -1;
+    p.y = static_cast<uint16_t*>(y);
+    p.y_stride = res_stride;
+    launch_epi<EPI_RESADD>(dtype, mt, waves, grid, stream, p);
   } else {
-    if (waves == 8)
-      launch_skinny<_Float16, 8, 8>(mt, grid, stream, yo, xi, wi, ri, M, N, K, x_stride, y_stride,
-                                    res_stride);
-    else
-      launch_skinny<_Float16, 4, 8>(mt, grid, stream, yo, xi, wi, ri, M, N, K, x_stride, y_stride,
-                                    res_stride);
+    p.y = static_cast<uint16_t*>(y);
+    p.y_stride = y_stride;
+    launch_epi<EPI_PLAIN>(dtype, mt, waves, grid, stream, p);
   }
+  return static_cast<int>(hipGetLastError());
+}
+
+int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x, const void* w,
+                        const int* positions, const int* slots, const float* cos_sin, int M,
+                        int K, int64_t x_stride, int64_t q_stride, int n_q_heads, int n_kv_heads,
+                        int block_size, float eps, int waves, int dtype, hipStream_t stream) {
+  if (waves != 4 && waves != 8) waves = 8;
+  if (skinny_checks(M, K, waves)) return -1;
+  int shift = 0;
+  while ((1 << shift) < block_size) ++shift;
+  if ((1 << shift) != block_size) return -1;
+  SkinnyParams p{};
+  p.x = static_cast<const uint16_t*>(x);
+  p.w = static_cast<const uint16_t*>(w);
+  p.y = static_cast<uint16_t*>(q_out);
+  p.x_stride = x_stride;
+  p.y_stride = q_stride;
+  p.M = M;
+  p.K = K;
+  p.N = (n_q_heads + 2 * n_kv_heads) * 128;
+  p.eps = eps;
+  p.k_cache = static_cast<uint16_t*>(k_cache);
+  p.v_cache = static_cast<uint16_t*>(v_cache);
+  p.positions = positions;
+  p.slots = slots;
+  p.cos_sin = cos_sin;
+  p.n_q_heads = n_q_heads;
+  p.n_kv_heads = n_kv_heads;
+  p.bs_shift = shift;
+  dim3 grid(p.N / 16);
+  launch_epi<EPI_QKVROPE>(dtype, M <= 16 ? 1 : 2, waves, grid, stream, p);
+  return static_cast<int>(hipGetLastError());
+}
+
+int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int K, int inter,
+                            int64_t x_stride, int64_t out_stride, float eps, int waves, int dtype,
+                            hipStream_t stream) {
+  if (waves != 4 && waves != 8) waves = 8;
+  if (skinny_checks(M, K, waves) || inter % 8 != 0) return -1;
+  SkinnyParams p{};
+  p.x = static_cast<const uint16_t*>(x);
+  p.w = static_cast<const uint16_t*>(w);
+  p.y = static_cast<uint16_t*>(out);
+  p.x_stride = x_stride;
+  p.y_stride = out_stride;
+  p.M = M;
+  p.K = K;
+  p.N = 2 * inter;
+  p.inter = inter;
+  p.eps = eps;
+  dim3 grid(inter / 8);
+  launch_epi<EPI_SILU>(dtype, M <= 16 ? 1 : 2, waves, grid, stream, p);
+  return static_cast<int>(hipGetLastError());
+}
+
+int atta_fused_lm_head_sample(int64_t* tokens, unsigned long long* keys, const void* x,
+                              const void* w, int M, int N, int K, int64_t x_stride, float eps,
+                              const float* temperature, const int64_t* seeds,
+                              const int64_t* steps, int finalize, int waves, int dtype,
+                              hipStream_t stream) {
+  if (waves != 4 && waves != 8) waves = 8;
+  if (skinny_checks(M, K, waves) || N % 16 != 0) return -1;
+  SkinnyParams p{};
+  p.x = static_cast<const uint16_t*>(x);
+  p.w = static_cast<const uint16_t*>(w);
+  p.x_stride = x_stride;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.eps = eps;
+  p.keys = keys;
+  p.temperature = temperature;
+  p.seeds = seeds;
+  p.steps = steps;
+  dim3 grid(N / 16);
+  launch_epi<EPI_SAMPLE>(dtype, M <= 16 ? 1 : 2, waves, grid, stream, p);
+  if (finalize) sample_finalize_kernel<<<(M + 63) / 64, 64, 0, stream>>>(tokens, keys, M);
+  return static_cast<int>(hipGetLastError());
+}
+
+// Tuning sweep entry: plain GEMM with a selectable (waves, unroll, load policy) variant.
+int atta_skinny_variant(void* y, const void* x, const void* w, int M, int N, int K,
+                        int variant, hipStream_t stream) {
+  SkinnyParams p{};
+  p.x = static_cast<const uint16_t*>(x);
+  p.w = static_cast<const uint16_t*>(w);
+  p.y = static_cast<uint16_t*>(y);
+  p.x_stride = K;
+  p.y_stride = N;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  if (M < 1 || M > 16 || N % 16) return -1;
+  dim3 grid(N / 16);
+  static const int waves_of[8] = {8, 8, 4, 4, 8, 16, 8, 16};
+  if (K % (32 * waves_of[variant & 7])) return -1;
+  switch (variant) {
+    case 0: skinny_kernel<__bf16, 8, 4, 1, EPI_PLAIN, true><<<grid, 512, 0, stream>>>(p); break;
+    case 1: skinny_kernel<__bf16, 8, 8, 1, EPI_PLAIN, true><<<grid, 512, 0, stream>>>(p); break;
+    case 2: skinny_kernel<__bf16, 4, 4, 1, EPI_PLAIN, true><<<grid, 256, 0, stream>>>(p); break;
+    case 3: skinny_kernel<__bf16, 4, 8, 1, EPI_PLAIN, true><<<grid, 256, 0, stream>>>(p); break;
+    case 4: skinny_kernel<__bf16, 8, 4, 1, EPI_PLAIN, false><<<grid, 512, 0, stream>>>(p); break;
+    case 5: skinny_kernel<__bf16, 16, 4, 1, EPI_PLAIN, true><<<grid, 1024, 0, stream>>>(p); break;
+    case 6: skinny_kernel<__bf16, 8, 2, 1, EPI_PLAIN, true><<<grid, 512, 0, stream>>>(p); break;
+    case 7: skinny_kernel<__bf16, 16, 2, 1, EPI_PLAIN, true><<<grid, 1024, 0, stream>>>(p); break;
+    default: return -1;
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+int atta_sample_finalize(int64_t* tokens, unsigned long long* keys, int M, hipStream_t stream) {
+  sample_finalize_kernel<<<(M + 63) / 64, 64, 0, stream>>>(tokens, keys, M);
   return static_cast<int>(hipGetLastError());
 }

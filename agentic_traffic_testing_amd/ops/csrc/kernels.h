@@ -39,3 +39,31 @@ int atta_sample(int64_t* out, const void* logits, int rows, int vocab, int64_t s
 int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual, int M, int N,
                      int K, int64_t x_stride, int64_t y_stride, int64_t res_stride, int waves,
                      int dtype, hipStream_t stream);
+
+int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x, const void* w,
+                        const int* positions, const int* slots, const float* cos_sin, int M,
+                        int K, int64_t x_stride, int64_t q_stride, int n_q_heads, int n_kv_heads,
+                        int block_size, float eps, int waves, int dtype, hipStream_t stream);
+
+int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int K, int inter,
+                            int64_t x_stride, int64_t out_stride, float eps, int waves, int dtype,
+                            hipStream_t stream);
+
+int atta_fused_lm_head_sample(int64_t* tokens, unsigned long long* keys, const void* x,
+                              const void* w, int M, int N, int K, int64_t x_stride, float eps,
+                              const float* temperature, const int64_t* seeds,
+                              const int64_t* steps, int finalize, int waves, int dtype,
+                              hipStream_t stream);
+
+int atta_sample_finalize(int64_t* tokens, unsigned long long* keys, int M, hipStream_t stream);
+
+int atta_attention_decode_v2(void* out, float* part_out, float* part_lse, int* counters,
+                             const void* q, const void* k_cache, const void* v_cache,
+                             const int* block_tables, const int* seq_kvlen, const int* seq_qstart,
+                             int num_seqs, int max_parts, int part_tokens, int n_q_heads,
+                             int n_kv_heads, int head_dim, int block_size, int bt_stride,
+                             int64_t q_stride, int64_t out_stride, float scale, int dtype,
+                             hipStream_t stream);
+
+int atta_skinny_variant(void* y, const void* x, const void* w, int M, int N, int K,
+                        int variant, hipStream_t stream);

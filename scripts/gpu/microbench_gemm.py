@@ -1,6 +1,14 @@
-"""Decode GEMM microbenchmark: MFMA skinny GEMM vs hipBLASLt (F.linear) at the Llama-3-8B
-decode shapes; reports us and effective HBM GB/s (weights streamed once)."""
+"""Decode-path microbenchmarks on MI355X.
+
+1. Skinny GEMM variants (waves x unroll x load policy) vs hipBLASLt (F.linear) at the
+   Llama-3-8B decode shapes; reports us and effective weight-stream GB/s.
+2. Decode attention: v1 (separate combine kernel) vs v2 (in-kernel combine) at the
+   contexts of the fan-out workload.
+Timings are medians of CUDA-event-timed loops over 4 rotating weight copies (so weights are
+not L2/MALL resident between calls)."""
+import math
 import os
+import statistics
 import sys
 
 import torch
@@ -10,29 +18,34 @@ from agentic_traffic_testing_amd import ops  # noqa: E402
 
 SHAPES = [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096),
           ("down", 4096, 14336), ("lm_head", 128256, 4096)]
+VARIANTS = {0: "w8u4", 1: "w8u8", 2: "w4u4", 3: "w4u8", 4: "w8u4-plain", 5: "w16u4",
+            6: "w8u2", 7: "w16u2"}
 
 
-def timeit(fn, iters=50):
+def timeit(fn, iters=40, reps=3):
     for _ in range(5):
         fn()
     torch.cuda.synchronize()
-    # rotate weights so they are not L2/MALL resident
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        fn()
-    e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / iters * 1000
+    res = []
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        res.append(s.elapsed_time(e) / iters * 1000)
+    return statistics.median(res)
 
 
-def main():
-    assert ops.native_available()
-    print(f"{'shape':>8} {'M':>3} {'blaslt_us':>10} {'GB/s':>7} {'skinny4_us':>11} {'GB/s':>7} {'skinny8_us':>11} {'GB/s':>7}")
+def gemm_sweep():
+    print("== skinny GEMM (us / GB/s)")
+    hdr = f"{'shape':>8} {'M':>3} {'blaslt':>13}" + "".join(f" {v:>15}" for v in VARIANTS.values())
+    print(hdr)
     for name, n, k in SHAPES:
         ws = [torch.randn(n, k, dtype=torch.bfloat16, device="cuda") * 0.02 for _ in range(4)]
         nbytes = n * k * 2
-        for m in (1, 5, 12, 16):
+        for m in (1, 5, 16):
             x = torch.randn(m, k, dtype=torch.bfloat16, device="cuda")
             out = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
             i = [0]
@@ -41,16 +54,53 @@ def main():
                 i[0] = (i[0] + 1) % 4
                 torch.nn.functional.linear(x, ws[i[0]])
 
-            def sk(waves):
-                def f():
-                    i[0] = (i[0] + 1) % 4
-                    torch.ops.atta.skinny_gemm(out, x, ws[i[0]], None, waves)
-                return f
             tb = timeit(blas)
-            t4 = timeit(sk(4))
-            t8 = timeit(sk(8))
-            print(f"{name:>8} {m:3d} {tb:10.1f} {nbytes / tb / 1e3:7.0f} {t4:11.1f} {nbytes / t4 / 1e3:7.0f} {t8:11.1f} {nbytes / t8 / 1e3:7.0f}", flush=True)
+            row = f"{name:>8} {m:3d} {tb:7.1f}/{nbytes / tb / 1e3:5.0f}"
+            for vid in VARIANTS:
+                def f(vid=vid):
+                    i[0] = (i[0] + 1) % 4
+                    torch.ops.atta.skinny_variant(out, x, ws[i[0]], vid)
+                try:
+                    t = timeit(f)
+                    row += f" {t:7.1f}/{nbytes / t / 1e3:5.0f}  "
+                except RuntimeError:
+                    row += f" {'n/a':>15}"
+            print(row, flush=True)
+
+
+def attn_sweep():
+    print("== decode attention (us): v1 = kernel + combine, v2 = in-kernel combine")
+    hq, hkv, bs = 32, 8, 16
+    for B, ctx in ((1, 300), (1, 600), (5, 500), (5, 1000), (1, 3800), (12, 2000)):
+        nblk = math.ceil(ctx / bs)
+        nb = B * nblk + 8
+        k = torch.randn(nb, hkv, bs, 128, dtype=torch.bfloat16, device="cuda")
+        v = torch.randn(nb, hkv, 128, bs, dtype=torch.bfloat16, device="cuda")
+        bt = torch.randperm(nb, device="cuda")[:B * nblk].view(B, nblk).to(torch.int32)
+        kvlen = torch.full((B,), ctx, dtype=torch.int32, device="cuda")
+        qstart = torch.arange(B + 1, dtype=torch.int32, device="cuda")
+        q = torch.randn(B, hq, 128, dtype=torch.bfloat16, device="cuda")
+        out = torch.empty_like(q)
+        row = f"B={B:2d} ctx={ctx:5d}"
+        for pt in (128, 256, 512):
+            mp = math.ceil(4096 / pt)
+            po = torch.empty(B * hkv * mp * 16 * 128, device="cuda")
+            pl = torch.empty(B * hkv * mp * 16, device="cuda")
+            cnt = torch.zeros(B * hkv, dtype=torch.int32, device="cuda")
+            t1 = timeit(lambda: ops.attention_decode(q, k, v, bt, kvlen, qstart, 0.088, po, pl,
+                                                     math.ceil(ctx / pt), pt, out=out))
+            t2 = timeit(lambda: ops.attention_decode_v2(q, k, v, bt, kvlen, qstart, 0.088, po, pl,
+                                                        cnt, mp, pt, out=out))
+            row += f" | pt={pt}: v1 {t1:6.1f} v2 {t2:6.1f}"
+        kv_bytes = B * ctx * hkv * 128 * 2 * 2
+        row += f" | ideal@6TB/s {kv_bytes / 6e6:5.1f}"
+        print(row, flush=True)
 
 
 if __name__ == "__main__":
-    main()
+    assert ops.native_available()
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what in ("all", "gemm"):
+        gemm_sweep()
+    if what in ("all", "attn"):
+        attn_sweep()

@@ -222,6 +222,96 @@ def test_skinny_gemm(dtype, m, n, k):
     got = ops.linear(x, w)
     close(got, exp, 2e-2 * math.sqrt(k / 4096), 1e-2)
     r = torch.randn(m, n, dtype=dtype, device="cuda")
-    got_r = ops.linear(x, w, residual=r)
     exp_r = (exp.to(dtype).float() + r.float())
+    got_r = ops.linear(x, w, residual=r)  # in place on r
+    assert got_r.data_ptr() == r.data_ptr()
     close(got_r, exp_r, 3e-2 * math.sqrt(k / 4096), 1e-2)
+
+
+def _norm_ref(x, eps=1e-5):
+    return ref.rms_norm(x, torch.ones(x.shape[1], dtype=x.dtype, device=x.device), eps)
+
+
+@pytest.mark.parametrize("m", [1, 5, 16, 24])
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (8, 1)])
+def test_decode_qkv_rope(m, hq, hkv):
+    torch.manual_seed(8)
+    dt, H, bs, nb = torch.bfloat16, 4096, 16, 64
+    x = torch.randn(m, H, dtype=dt, device="cuda") * 2
+    w = torch.randn((hq + 2 * hkv) * 128, H, dtype=dt, device="cuda") * 0.02
+    pos = torch.randint(0, 4000, (m,), dtype=torch.int32, device="cuda")
+    slots = torch.randperm(nb * bs, device="cuda")[:m].to(torch.int32)
+    if m > 1:
+        slots[1] = -1
+    cs = ref.rope_cos_sin(128, 8192, 500000.0, None, device="cuda")
+    k1, v1 = _rand_cache(nb, hkv, bs, 128, dt)
+    k2, v2 = k1.clone(), v1.clone()
+    qkv = torch.nn.functional.linear(_norm_ref(x), w)
+    q_exp = ref.rope_cache(qkv, pos, slots, cs, k1, v1, hq, hkv, 128)
+    q_got = ops.decode_qkv_rope(x, w, 1e-5, pos, slots, cs, k2, v2, hq, hkv)
+    close(q_got, q_exp, 3e-2, 2e-2)
+    close(k2, k1, 3e-2, 2e-2)
+    close(v2, v1, 3e-2, 2e-2)
+
+
+@pytest.mark.parametrize("m", [1, 5, 16, 32])
+@pytest.mark.parametrize("inter,k", [(14336, 4096), (2816, 1024)])
+def test_decode_gate_up_silu(m, inter, k):
+    torch.manual_seed(9)
+    dt = torch.bfloat16
+    x = torch.randn(m, k, dtype=dt, device="cuda")
+    w = torch.randn(2 * inter, k, dtype=dt, device="cuda") * 0.02
+    exp = ref.silu_and_mul(torch.nn.functional.linear(_norm_ref(x), w))
+    got = ops.decode_gate_up_silu(x, w, 1e-5)
+    # the kernel scales by 1/rms after the GEMM instead of rounding the normalised row to
+    # bf16 first; silu(g)*u then amplifies that last-bit difference
+    close(got, exp, 4e-2, 4e-2)
+
+
+@pytest.mark.parametrize("m", [1, 5, 12])
+def test_decode_lm_head_sample(m):
+    torch.manual_seed(10)
+    dt, V, H = torch.bfloat16, 32768, 1024
+    x = torch.randn(m, H, dtype=dt, device="cuda")
+    w = torch.randn(V, H, dtype=dt, device="cuda") * 0.05
+    keys = torch.zeros(32, dtype=torch.int64, device="cuda")
+    temp = torch.zeros(m, device="cuda")
+    seeds = torch.arange(m, dtype=torch.int64, device="cuda")
+    steps = torch.zeros(m, dtype=torch.int64, device="cuda")
+    logits = torch.nn.functional.linear(_norm_ref(x), w).float()
+    for _ in range(3):  # keys must re-arm between launches
+        got = ops.decode_lm_head_sample(x, w, 1e-5, temp, seeds, steps, keys)
+        top2 = torch.topk(logits, 2, dim=-1)
+        for r in range(m):
+            g = int(got[r])
+            # exact argmax unless the top-2 are within bf16 rounding of each other
+            assert g == int(top2.indices[r, 0]) or \
+                float(top2.values[r, 0] - logits[r, g]) < 0.05
+    assert bool((keys == 0).all())
+    temp.fill_(0.8)
+    toks = ops.decode_lm_head_sample(x, w, 1e-5, temp, seeds, steps, keys)
+    assert bool(((toks >= 0) & (toks < V)).all())
+
+
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (8, 1), (64, 8)])
+@pytest.mark.parametrize("part_tokens", [64, 256])
+def test_attention_decode_v2(hq, hkv, part_tokens):
+    torch.manual_seed(11)
+    dt, bs = torch.bfloat16, 16
+    seqs = [(1, 1), (17, 1), (256, 1), (1000, 1), (63, 1), (2048, 1), (0, 1)]
+    k, v, bt, kvlen, qstart, T = _make_paged([(max(kv, 1), q) for kv, q in seqs], hkv, bs, dt)
+    kvlen[-1] = 0  # dummy (graph padding) sequence
+    q = torch.randn(T, hq, 128, dtype=dt, device="cuda")
+    max_parts = math.ceil(4096 / part_tokens)
+    S = len(seqs)
+    po = torch.empty(S * hkv * max_parts * 16 * 128, device="cuda")
+    pl = torch.empty(S * hkv * max_parts * 16, device="cuda")
+    cnt = torch.zeros(S * hkv, dtype=torch.int32, device="cuda")
+    scale = 1 / math.sqrt(128)
+    exp = ref.paged_attention(q, k, v, bt.clamp(min=0), kvlen, qstart, scale)
+    for _ in range(3):  # counters must re-arm
+        out = torch.full_like(q, 3.0)
+        ops.attention_decode_v2(q, k, v, bt, kvlen, qstart, scale, po, pl, cnt, max_parts,
+                                part_tokens, out=out)
+        close(out[:-1], exp[:-1], 1.5e-2, 2e-2)
+        assert bool((cnt == 0).all())
