@@ -21,10 +21,16 @@ class MetricsLogger:
     _lock = threading.Lock()
 
     def __init__(self, log_dir: str | None = None):
-        log_dir = log_dir or os.environ.get("METRICS_LOG_DIR", "logs")
-        os.makedirs(log_dir, exist_ok=True)
-        self.log_file = os.path.join(log_dir, "llm_calls.jsonl")
-        self.model_name = os.environ.get("MODEL_NAME", "unknown")
+        self._fixed_dir = log_dir
+
+    @property
+    def log_file(self) -> str:
+        d = self._fixed_dir or os.environ.get("METRICS_LOG_DIR", "logs")
+        return os.path.join(d, "llm_calls.jsonl")
+
+    @property
+    def model_name(self) -> str:
+        return os.environ.get("MODEL_NAME", "unknown")
 
     def log_call(self, *, task_id: str, agent_id: str, call_type: str, timestamp_start: str,
                  timestamp_end: str, http_status: int, llm_meta: dict | None = None,
@@ -49,8 +55,10 @@ class MetricsLogger:
             "error": error,
         }
         line = json.dumps(rec, sort_keys=True, default=str)
+        path = self.log_file
         try:
-            with self._lock, open(self.log_file, "a", encoding="utf-8") as f:
+            os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+            with self._lock, open(path, "a", encoding="utf-8") as f:
                 f.write(line + "\n")
         except OSError as exc:
             print(f"[metrics-logger-error] {exc}: {line}", file=sys.stderr)

@@ -36,14 +36,26 @@ class TelemetryLogger:
         self.agent_id = agent_id
         self.scenario = scenario
         self.node_id = node_id()
-        log_dir = os.environ.get("TELEMETRY_LOG_DIR", "logs")
-        self.log_file = log_file or os.path.join(log_dir, f"{self.node_id}_{agent_id}.log")
-        d = os.path.dirname(self.log_file)
-        if d:
-            os.makedirs(d, exist_ok=True)
+        self._fixed_file = log_file
+
+    @property
+    def log_file(self) -> str:
+        """Resolved per call so TELEMETRY_LOG_DIR changes (tests, stacks) take effect."""
+        if self._fixed_file:
+            return self._fixed_file
+        return os.path.join(os.environ.get("TELEMETRY_LOG_DIR", "logs"),
+                            f"{self.node_id}_{self.agent_id}.log")
+
+    @staticmethod
+    def _lock_for(path: str) -> threading.Lock:
         with TelemetryLogger._locks_guard:
-            self._lock = TelemetryLogger._locks.setdefault(os.path.abspath(self.log_file),
-                                                           threading.Lock())
+            lk = TelemetryLogger._locks.get(path)
+            if lk is None:
+                d = os.path.dirname(path)
+                if d:
+                    os.makedirs(d, exist_ok=True)
+                lk = TelemetryLogger._locks[path] = threading.Lock()
+            return lk
 
     @staticmethod
     def new_task_id() -> str:
@@ -67,8 +79,9 @@ class TelemetryLogger:
             "node_id": self.node_id,
         }
         line = json.dumps(rec, sort_keys=True, default=str)
+        path = self.log_file
         try:
-            with self._lock, open(self.log_file, "a", encoding="utf-8") as f:
+            with self._lock_for(os.path.abspath(path)), open(path, "a", encoding="utf-8") as f:
                 f.write(line + "\n")
         except OSError as exc:
             print(f"[telemetry-error] {exc}: {line}", file=sys.stderr)

@@ -76,6 +76,9 @@ class LLMEngine:
         self.total_generated = 0
         self.total_prompt = 0
         self.batch_size_history: list = []
+        # host-side step breakdown (seconds): scheduler, runner.execute (prep + GPU + sync),
+        # output processing
+        self.timing = {"schedule": 0.0, "execute": 0.0, "post": 0.0, "steps": 0}
         self._rng = random.Random(cfg.seed)
 
     # ------------------------------------------------------------------------------------
@@ -105,12 +108,16 @@ class LLMEngine:
     # ------------------------------------------------------------------------------------
     def step(self) -> list[RequestOutput]:
         with self.lock:
+            ts = time.perf_counter()
             batch = self.scheduler.schedule()
             if batch.empty:
                 return []
             t0 = time.perf_counter()
             toks = self.runner.execute(batch)
             now = time.perf_counter()
+            self.timing["schedule"] += t0 - ts
+            self.timing["execute"] += now - t0
+            self.timing["steps"] += 1
             outs = []
             for seq, n, tok in zip(batch.seqs, batch.q_len, toks):
                 seq.num_computed += n
@@ -133,6 +140,7 @@ class LLMEngine:
             self.batch_size_history.append(len(batch.seqs))
             if len(self.batch_size_history) > 4096:
                 del self.batch_size_history[:2048]
+            self.timing["post"] += time.perf_counter() - now
             return outs
 
     def _stop_reason(self, seq: Sequence, tok: int) -> str | None:

@@ -150,6 +150,7 @@ class ModelRunner:
         self.graph_pool = None
         self.steps = 0
         self.graph_steps = 0
+        self.timing = {"graph_prep": 0.0, "graph_run": 0.0}
 
     # ------------------------------------------------------------------------------------
     def _alloc_kv(self):
@@ -254,12 +255,17 @@ class ModelRunner:
             if bucket not in self.graphs:
                 self.capture(bucket)
             io = self.graph_io[bucket]
+            t0 = time.perf_counter()
             lay, arrays = self._prepare(batch, pad_seqs=bucket, tiles=False)
             assert lay.size == io["layout"].size
             self._upload(lay, arrays, io["dev"])
+            t1 = time.perf_counter()
             self.graphs[bucket].replay()
             self.graph_steps += 1
-            return io["out"][:n].cpu().numpy()
+            out = io["out"][:n].cpu().numpy()
+            self.timing["graph_prep"] += t1 - t0
+            self.timing["graph_run"] += time.perf_counter() - t1
+            return out
         lay, arrays = self._prepare(batch)
         v = self._upload(lay, arrays)
         md = self._meta(v, batch.num_decode, lay.NT)

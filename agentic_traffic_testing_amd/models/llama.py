@@ -259,7 +259,7 @@ class LlamaModel:
         return ops.fused_add_rms_norm(h, residual, self.norm, eps)
 
     def decode_fusable(self, num_tokens: int) -> bool:
-        step = 32 * ops.SKINNY_WAVES
+        step = 128
         return (self.device.type == "cuda" and num_tokens <= ops.SKINNY_MAX_M
                 and self.cfg.hidden_size % step == 0 and self.inter % step == 0
                 and (self.n_heads * self.head_dim) % step == 0)
@@ -287,12 +287,13 @@ class LlamaModel:
                                     ws["part_lse"], ws["counters"], ws["max_parts"],
                                     ws["part_tokens"], out=attn, num_seqs=B)
             if self.tp_size == 1:
-                ops.linear(attn.view(B, nq * self.head_dim), L.o, residual=residual)
+                ops.linear(attn.view(B, nq * self.head_dim), L.o, residual=residual,
+                           waves=ops.WAVES_SMALL)
             else:
                 residual.add_(self._all_reduce(ops.linear(attn.view(B, nq * self.head_dim), L.o)))
             ops.decode_gate_up_silu(residual, L.gate_up, eps, out=act)
             if self.tp_size == 1:
-                ops.linear(act, L.down, residual=residual)
+                ops.linear(act, L.down, residual=residual, waves=ops.WAVES_LARGE)
             else:
                 residual.add_(self._all_reduce(ops.linear(act, L.down)))
         if self.tp_size == 1:

@@ -156,26 +156,30 @@ PREFILL_TILE_TOKENS = {1: 64, 2: 32, 4: 16, 8: 8}  # tokens per prefill workgrou
 # larger M (prefill) goes to hipBLASLt through F.linear.
 SKINNY_MAX_M = int(os.environ.get("ATTA_SKINNY_MAX_M", "32"))
 SKINNY_WAVES = int(os.environ.get("ATTA_SKINNY_WAVES", "8"))
+# per-projection wave counts from the MI355X sweep (profiles/r1_microbench_v3_plain.txt):
+# 8 waves x 2-deep stages for the small qkv / o projections, 16 waves for the large ones.
+WAVES_SMALL = int(os.environ.get("ATTA_WAVES_SMALL", "8"))
+WAVES_LARGE = int(os.environ.get("ATTA_WAVES_LARGE", "16"))
 
 
 def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
     m, k = x.shape
     return (x.is_cuda and 1 <= m <= SKINNY_MAX_M and w.shape[0] % 16 == 0
-            and k % (32 * SKINNY_WAVES) == 0 and x.stride(1) == 1 and w.is_contiguous())
+            and k % 128 == 0 and x.stride(1) == 1 and w.is_contiguous())
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None,
-           out: torch.Tensor | None = None) -> torch.Tensor:
+           out: torch.Tensor | None = None, waves: int | None = None) -> torch.Tensor:
     """y = x @ w.T.  With ``residual`` the product is added to ``residual`` IN PLACE and
     ``residual`` is returned (residual-stream update).  Decode-sized M runs the MFMA skinny
     GEMM; everything else (prefill, CPU) runs F.linear (hipBLASLt on the GPU)."""
     if skinny_ok(x, w):
         if residual is not None:
-            _native().skinny_gemm(residual, x, w, residual, SKINNY_WAVES)
+            _native().skinny_gemm(residual, x, w, residual, waves or SKINNY_WAVES)
             return residual
         if out is None:
             out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
-        _native().skinny_gemm(out, x, w, None, SKINNY_WAVES)
+        _native().skinny_gemm(out, x, w, None, waves or SKINNY_WAVES)
         return out
     y = torch.nn.functional.linear(x, w)
     if residual is not None:
@@ -200,7 +204,7 @@ def decode_qkv_rope(x, w, eps, positions, slots, cos_sin, k_cache, v_cache, n_q_
         q_out.copy_(q)
         return q_out
     _native().fused_qkv_rope(q_out, k_cache, v_cache, x, w, positions, slots, cos_sin,
-                             n_q_heads, n_kv_heads, eps, SKINNY_WAVES)
+                             n_q_heads, n_kv_heads, eps, WAVES_SMALL)
     return q_out
 
 
@@ -213,7 +217,7 @@ def decode_gate_up_silu(x, w, eps, out=None):
         n = ref.rms_norm(x, torch.ones(x.shape[1], dtype=x.dtype), eps)
         out.copy_(ref.silu_and_mul(torch.nn.functional.linear(n, w)))
         return out
-    _native().fused_gate_up_silu(out, x, w, eps, SKINNY_WAVES)
+    _native().fused_gate_up_silu(out, x, w, eps, WAVES_LARGE)
     return out
 
 
@@ -228,7 +232,7 @@ def decode_lm_head_sample(x, w, eps, temperature, seeds, steps, keys, tokens=Non
         tokens.copy_(ref.sample(torch.nn.functional.linear(n, w), temperature, seeds, steps))
         return tokens
     _native().fused_lm_head_sample(tokens, keys, x, w, eps, temperature, seeds, steps, finalize,
-                                   SKINNY_WAVES)
+                                   WAVES_LARGE)
     return tokens
 
 

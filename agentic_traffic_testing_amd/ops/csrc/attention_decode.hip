@@ -1,18 +1,22 @@
-// Decode paged attention v2: split-K over context partitions with an in-kernel combine
+// Decode paged attention: split-K over context partitions with an in-kernel combine
 // (guide §5 "In-launch split-K reduction").
 //
-// grid = (seqs, kv_heads, max_partitions), 4 waves per workgroup.  One workgroup handles
-// `part_tokens` tokens of one (sequence, KV head); its 4 waves take every 4th 16-token tile
-// and keep the next tile's K/V fragments in flight while computing the current one
-// (register double buffer).  The GQA group's G query heads are the MFMA columns (same
-// swapped-QK^T formulation as attention.hip).  Partitions past the sequence end exit at
-// once, so a hipGraph captured with the maximum partition count costs nothing extra for
-// short contexts.
+// grid = (seqs, kv_heads, max_partitions); a workgroup of WAVES waves owns one partition of
+// WAVES * 16 * TPW tokens of one (sequence, KV head).  Decode attention at agent-workload
+// sizes is LATENCY bound (a few MB of KV per layer), so the kernel minimises dependent
+// memory round trips per wave:
+//   1. Q fragment + the block-table entries of the wave's TPW tiles are loaded together;
+//   2. the K/V fragments of ALL the wave's tiles are issued at once (no per-tile
+//      block-table -> K/V dependency chain);
+//   3. online softmax + PV over the tiles, one LDS merge of the WAVES partial states.
+// The GQA group's G query heads are the MFMA columns (swapped QK^T, see attention.hip), so
+// K/V are read once for all G heads.  Partitions past the sequence end exit immediately,
+// so a hipGraph captured with the maximum partition count costs nothing for short contexts.
 //
-// Combine: every partition writes (O normalised, lse) fp32 to a workspace, then arrives on
-// a per-(seq, kv-head) counter with an agent-scope release; the last arriver acquires,
-// merges all partitions and writes the bf16 output, then re-arms the counter (counters are
-// zeroed once at allocation).  A context that fits one partition skips the workspace.
+// Combine: with more than one partition each workgroup writes (O normalised, lse) fp32 to a
+// workspace and arrives on a per-(seq, kv-head) counter (agent-scope release); the last
+// arriver acquires, merges every partition and writes the bf16 output, then re-arms the
+// counter (counters are zeroed once at allocation).
 #include "common.h"
 #include "kernels.h"
 
@@ -68,71 +72,13 @@ struct TileFrags {
   i16x4 v[8];
 };
 
-template <typename T>
-__device__ __forceinline__ void load_tile(TileFrags<T>& f, const DecParams& p, const int* bt,
-                                          int kt, int kvlen, int hk, int col, int grp) {
+template <typename T, int G, int WAVES, int TPW>
+__global__ __launch_bounds__(WAVES * 64) void decode_attention_kernel(DecParams p) {
   using frag8 = typename Mf<T>::frag8;
-  const int BS = 1 << p.bs_shift;
-  const int64_t hs = static_cast<int64_t>(BS) * kD;
-  const int tk = kt + col;
-  const int pk = tk < kvlen ? bt[tk >> p.bs_shift] : 0;
-  const uint16_t* kp = p.k_cache + (static_cast<int64_t>(pk) * p.n_kv_heads + hk) * hs +
-                       static_cast<int64_t>(tk & (BS - 1)) * kD + 32 * grp;
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) f.k[kk] = *reinterpret_cast<const frag8*>(kp + 8 * kk);
-  const int tv = kt + 4 * grp;
-  const int pv = tv < kvlen ? bt[tv >> p.bs_shift] : 0;
-  const uint16_t* vp = p.v_cache + (static_cast<int64_t>(pv) * p.n_kv_heads + hk) * hs +
-                       static_cast<int64_t>(col) * BS + (tv & (BS - 1));
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt)
-    f.v[dt] = *reinterpret_cast<const i16x4*>(vp + static_cast<int64_t>(16 * dt) * BS);
-}
-
-template <typename T>
-__device__ __forceinline__ void compute_tile(const TileFrags<T>& f,
-                                             const typename Mf<T>::frag8 (&qf)[4], int kt,
-                                             int kv_end, int grp, float scale_log2, float& m_run,
-                                             float& l_run, f32x4 (&o)[8]) {
-  f32x4 s = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) s = Mf<T>::qk(f.k[kk], qf[kk], s);
-  float sv[4], tmax = kNegInf;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    sv[i] = (kt + 4 * grp + i < kv_end) ? s[i] * scale_log2 : kNegInf;
-    tmax = fmaxf(tmax, sv[i]);
-  }
-  tmax = fmaxf(tmax, __shfl_xor(tmax, 16, kWave));
-  tmax = fmaxf(tmax, __shfl_xor(tmax, 32, kWave));
-  const float m_new = fmaxf(m_run, tmax);
-  const float m_use = (m_new == kNegInf) ? 0.f : m_new;
-  const float alpha = exp2f(m_run - m_use);
-  float psum = 0.f;
-  i16x4 pf;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float pv = exp2f(sv[i] - m_use);
-    psum += pv;
-    pf[i] = static_cast<short>(from_f32<T>(pv));
-  }
-  psum += __shfl_xor(psum, 16, kWave);
-  psum += __shfl_xor(psum, 32, kWave);
-  l_run = l_run * alpha + psum;
-  m_run = m_new;
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) {
-    o[dt] *= alpha;
-    o[dt] = Mf<T>::pv(f.v[dt], pf, o[dt]);
-  }
-}
-
-template <typename T, int G>
-__global__ __launch_bounds__(256) void decode_attention_kernel(DecParams p) {
-  using frag8 = typename Mf<T>::frag8;
-  __shared__ float lds_o[4][16][kD + 4];
-  __shared__ float lds_m[4][16];
-  __shared__ float lds_l[4][16];
+  __shared__ float lds_o[WAVES][G][kD + 4];
+  __shared__ float lds_m[WAVES][G];
+  __shared__ float lds_l[WAVES][G];
+  __shared__ float lds_w[64][G];
   __shared__ int lds_last;
 
   const int lane = threadIdx.x & 63;
@@ -143,13 +89,16 @@ __global__ __launch_bounds__(256) void decode_attention_kernel(DecParams p) {
   const int hk = blockIdx.y;
   const int part = blockIdx.z;
   const int kvlen = p.seq_kvlen[s];
-  const int nparts = (kvlen + p.part_tokens - 1) / p.part_tokens;
-  if (part >= nparts) return;  // block-uniform; also covers kvlen == 0 dummy sequences
-  const int kv_begin = part * p.part_tokens;
-  const int kv_end = min(kvlen, kv_begin + p.part_tokens);
+  const int PT = WAVES * 16 * TPW;
+  const int nparts = (kvlen + PT - 1) / PT;
+  if (part >= nparts) return;  // block-uniform (also kvlen == 0 dummy sequences)
+  const int kv_begin = part * PT;
+  const int kv_end = min(kvlen, kv_begin + PT);
   const int qrow = p.seq_qstart[s + 1] - 1;
+  const int BS = 1 << p.bs_shift;
+  const int64_t hs = static_cast<int64_t>(BS) * kD;
 
-  // Q fragment: column = GQA head (col < G), dims 32*grp + 8*kk + j
+  // ---- round trip 1: Q fragment + block-table entries of this wave's tiles -------------
   frag8 qf[4];
   {
     const bool ok = col < G;
@@ -159,67 +108,110 @@ __global__ __launch_bounds__(256) void decode_attention_kernel(DecParams p) {
     for (int kk = 0; kk < 4; ++kk)
       qf[kk] = ok ? *reinterpret_cast<const frag8*>(qp + 8 * kk) : frag8{};
   }
+  const int* bt = p.block_tables + static_cast<int64_t>(s) * p.bt_stride;
+  int page[TPW];
+  int kt[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    kt[i] = kv_begin + (wid + i * WAVES) * 16;
+    page[i] = kt[i] < kv_end ? bt[kt[i] >> p.bs_shift] : 0;
+  }
+
+  // ---- round trip 2: K/V fragments of all tiles -----------------------------------------
+  TileFrags<T> f[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    if (kt[i] < kv_end) {
+      const uint16_t* base = p.k_cache + (static_cast<int64_t>(page[i]) * p.n_kv_heads + hk) * hs;
+      const uint16_t* kp = base + static_cast<int64_t>((kt[i] + col) & (BS - 1)) * kD + 32 * grp;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) f[i].k[kk] = *reinterpret_cast<const frag8*>(kp + 8 * kk);
+      const uint16_t* vb = p.v_cache + (static_cast<int64_t>(page[i]) * p.n_kv_heads + hk) * hs;
+      const uint16_t* vp = vb + static_cast<int64_t>(col) * BS + ((kt[i] + 4 * grp) & (BS - 1));
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+        f[i].v[dt] = *reinterpret_cast<const i16x4*>(vp + static_cast<int64_t>(16 * dt) * BS);
+    }
+  }
+
+  // ---- compute --------------------------------------------------------------------------
   f32x4 o[8];
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_run = kNegInf, l_run = 0.f;
-  const int* bt = p.block_tables + static_cast<int64_t>(s) * p.bt_stride;
-
-  int kt = kv_begin + wid * 16;
-  if (kt < kv_end) {
-    TileFrags<T> fa, fb;
-    load_tile<T>(fa, p, bt, kt, kvlen, hk, col, grp);
-    while (true) {
-      const int kn = kt + 64;
-      if (kn < kv_end) load_tile<T>(fb, p, bt, kn, kvlen, hk, col, grp);
-      compute_tile<T>(fa, qf, kt, kv_end, grp, p.scale_log2, m_run, l_run, o);
-      if (kn >= kv_end) break;
-      const int kn2 = kn + 64;
-      if (kn2 < kv_end) load_tile<T>(fa, p, bt, kn2, kvlen, hk, col, grp);
-      compute_tile<T>(fb, qf, kn, kv_end, grp, p.scale_log2, m_run, l_run, o);
-      if (kn2 >= kv_end) break;
-      kt = kn2;
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    if (kt[i] >= kv_end) break;  // wave-uniform
+    f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) sacc = Mf<T>::qk(f[i].k[kk], qf[kk], sacc);
+    float sv[4], tmax = kNegInf;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sv[j] = (kt[i] + 4 * grp + j < kv_end) ? sacc[j] * p.scale_log2 : kNegInf;
+      tmax = fmaxf(tmax, sv[j]);
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, kWave));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, kWave));
+    const float m_new = fmaxf(m_run, tmax);
+    const float m_use = (m_new == kNegInf) ? 0.f : m_new;
+    const float alpha = exp2f(m_run - m_use);
+    float psum = 0.f;
+    i16x4 pf;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float pv = exp2f(sv[j] - m_use);
+      psum += pv;
+      pf[j] = static_cast<short>(from_f32<T>(pv));
+    }
+    psum += __shfl_xor(psum, 16, kWave);
+    psum += __shfl_xor(psum, 32, kWave);
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      o[dt] *= alpha;
+      o[dt] = Mf<T>::pv(f[i].v[dt], pf, o[dt]);
     }
   }
 
-  // ---- merge the 4 waves -----------------------------------------------------------------
+  // ---- merge the WAVES partial states (only the G valid columns) ---------------------------
+  if (col < G) {
 #pragma unroll
-  for (int dt = 0; dt < 8; ++dt)
+    for (int dt = 0; dt < 8; ++dt)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) lds_o[wid][col][16 * dt + 4 * grp + i] = o[dt][i];
-  if (grp == 0) {
-    lds_m[wid][col] = m_run;
-    lds_l[wid][col] = l_run;
+      for (int j = 0; j < 4; ++j) lds_o[wid][col][16 * dt + 4 * grp + j] = o[dt][j];
+    if (grp == 0) {
+      lds_m[wid][col] = m_run;
+      lds_l[wid][col] = l_run;
+    }
   }
   __syncthreads();
-  const int c = threadIdx.x >> 4;         // column 0..15
-  const int d0 = (threadIdx.x & 15) * 8;  // dims d0..d0+7
-  float mw[4], mx = kNegInf;
+  const bool merger = threadIdx.x < G * 16;
+  const int c = threadIdx.x >> 4;          // column (query head in the group)
+  const int d0 = (threadIdx.x & 15) * 8;   // dims d0..d0+7
+  float r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float mu = 0.f, L = 0.f;
+  if (merger) {
+    float mx = kNegInf;
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    mw[w] = lds_m[w][c];
-    mx = fmaxf(mx, mw[w]);
-  }
-  const float mu = (mx == kNegInf) ? 0.f : mx;
-  float L = 0.f, fw[4];
+    for (int w = 0; w < WAVES; ++w) mx = fmaxf(mx, lds_m[w][c]);
+    mu = (mx == kNegInf) ? 0.f : mx;
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    fw[w] = exp2f(mw[w] - mu);
-    L += fw[w] * lds_l[w][c];
-  }
-  const float invL = L > 0.f ? 1.f / L : 0.f;
-  float r[8];
+    for (int w = 0; w < WAVES; ++w) {
+      const float fw = exp2f(lds_m[w][c] - mu);
+      L += fw * lds_l[w][c];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float a = 0.f;
+      for (int j = 0; j < 8; ++j) r[j] += fw * lds_o[w][c][d0 + j];
+    }
+    const float invL = L > 0.f ? 1.f / L : 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) a += fw[w] * lds_o[w][c][d0 + j];
-    r[j] = a * invL;
+    for (int j = 0; j < 8; ++j) r[j] *= invL;
   }
   uint16_t* outp = p.out + static_cast<int64_t>(qrow) * p.out_stride +
                    static_cast<int64_t>(hk * G + c) * kD + d0;
   if (nparts == 1) {
-    if (c < G) {
+    if (merger) {
       Pack8 o8;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o8.v[j] = from_f32<T>(r[j]);
@@ -228,9 +220,9 @@ __global__ __launch_bounds__(256) void decode_attention_kernel(DecParams p) {
     return;
   }
 
-  // ---- publish this partition, last arriver combines ----------------------------------------
+  // ---- publish this partition; the last arriver combines -----------------------------------
   const int64_t sh = static_cast<int64_t>(s) * p.n_kv_heads + hk;
-  if (c < G) {
+  if (merger) {
     const int64_t base = (sh * p.max_parts + part) * 16 + c;
     float* po = p.part_out + base * kD + d0;
     *reinterpret_cast<float4*>(po) = make_float4(r[0], r[1], r[2], r[3]);
@@ -253,21 +245,25 @@ __global__ __launch_bounds__(256) void decode_attention_kernel(DecParams p) {
   }
   __syncthreads();
   if (!lds_last) return;
-  if (c < G) {
+  // partition weights: lds_w[q][c] = 2^(lse_q - lse_max)
+  const int np = min(nparts, 64);
+  for (int e = threadIdx.x; e < np * G; e += WAVES * 64) {
+    const int q = e / G, cc = e % G;
+    lds_w[q][cc] = p.part_lse[(sh * p.max_parts + q) * 16 + cc];
+  }
+  __syncthreads();
+  if (merger) {
     float lmax = kNegInf;
-    for (int q = 0; q < nparts; ++q)
-      lmax = fmaxf(lmax, p.part_lse[(sh * p.max_parts + q) * 16 + c]);
+    for (int q = 0; q < np; ++q) lmax = fmaxf(lmax, lds_w[q][c]);
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float wsum = 0.f;
     if (lmax != kNegInf) {
-      for (int q = 0; q < nparts; ++q) {
+      for (int q = 0; q < np; ++q) {
+        const float w = exp2f(lds_w[q][c] - lmax);  // lse == -inf -> weight 0
         const int64_t base = (sh * p.max_parts + q) * 16 + c;
-        const float l = p.part_lse[base];
-        if (l == kNegInf) continue;
-        const float w = exp2f(l - lmax);
-        wsum += w;
         const float4 a = *reinterpret_cast<const float4*>(p.part_out + base * kD + d0);
         const float4 b = *reinterpret_cast<const float4*>(p.part_out + base * kD + d0 + 4);
+        wsum += w;
         acc[0] += w * a.x; acc[1] += w * a.y; acc[2] += w * a.z; acc[3] += w * a.w;
         acc[4] += w * b.x; acc[5] += w * b.y; acc[6] += w * b.z; acc[7] += w * b.w;
       }
@@ -282,15 +278,26 @@ __global__ __launch_bounds__(256) void decode_attention_kernel(DecParams p) {
     __hip_atomic_store(p.counters + sh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <typename T>
-static void launch(int G, dim3 grid, hipStream_t st, const DecParams& p) {
+template <typename T, int WAVES, int TPW>
+static int launch_g(int G, dim3 grid, hipStream_t st, const DecParams& p) {
   switch (G) {
-    case 1: decode_attention_kernel<T, 1><<<grid, 256, 0, st>>>(p); break;
-    case 2: decode_attention_kernel<T, 2><<<grid, 256, 0, st>>>(p); break;
-    case 4: decode_attention_kernel<T, 4><<<grid, 256, 0, st>>>(p); break;
-    case 8: decode_attention_kernel<T, 8><<<grid, 256, 0, st>>>(p); break;
-    case 16: decode_attention_kernel<T, 16><<<grid, 256, 0, st>>>(p); break;
-    default: break;
+    case 1: decode_attention_kernel<T, 1, WAVES, TPW><<<grid, WAVES * 64, 0, st>>>(p); return 0;
+    case 2: decode_attention_kernel<T, 2, WAVES, TPW><<<grid, WAVES * 64, 0, st>>>(p); return 0;
+    case 4: decode_attention_kernel<T, 4, WAVES, TPW><<<grid, WAVES * 64, 0, st>>>(p); return 0;
+    case 8: decode_attention_kernel<T, 8, WAVES, TPW><<<grid, WAVES * 64, 0, st>>>(p); return 0;
+    default: return -1;
+  }
+}
+
+// part_tokens selects the workgroup shape: 128 = 4 waves x 2 tiles, 256 = 8 x 2,
+// 512 = 16 x 2 (16 waves cap VGPRs at 128: more tiles per wave would spill).
+template <typename T>
+static int launch(int G, int part_tokens, dim3 grid, hipStream_t st, const DecParams& p) {
+  switch (part_tokens) {
+    case 128: return launch_g<T, 4, 2>(G, grid, st, p);
+    case 256: return launch_g<T, 8, 2>(G, grid, st, p);
+    case 512: return launch_g<T, 16, 2>(G, grid, st, p);
+    default: return -1;
   }
 }
 
@@ -310,8 +317,8 @@ int atta_attention_decode_v2(void* out, float* part_out, float* part_lse, int* c
   int shift = 0;
   while ((1 << shift) < block_size) ++shift;
   if (head_dim != 128 || (1 << shift) != block_size || block_size < 16) return -1;
-  if (n_q_heads % n_kv_heads || G > 16 || (G & (G - 1))) return -1;
-  if (part_tokens % 64 != 0 || max_parts < 1) return -1;
+  if (n_q_heads % n_kv_heads || G > 8 || (G & (G - 1))) return -1;
+  if (max_parts < 1 || max_parts > 64) return -1;
   if (num_seqs == 0) return 0;
   dec::DecParams p{};
   p.out = static_cast<uint16_t*>(out);
@@ -333,9 +340,8 @@ int atta_attention_decode_v2(void* out, float* part_out, float* part_lse, int* c
   p.max_parts = max_parts;
   p.scale_log2 = scale * 1.4426950408889634f;
   dim3 grid(num_seqs, n_kv_heads, max_parts);
-  if (dtype == 0)
-    dec::launch<__bf16>(G, grid, stream, p);
-  else
-    dec::launch<_Float16>(G, grid, stream, p);
+  const int rc = dtype == 0 ? dec::launch<__bf16>(G, part_tokens, grid, stream, p)
+                            : dec::launch<_Float16>(G, part_tokens, grid, stream, p);
+  if (rc) return rc;
   return static_cast<int>(hipGetLastError());
 }

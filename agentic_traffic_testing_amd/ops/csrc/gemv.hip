@@ -113,7 +113,7 @@ __device__ __forceinline__ int tile_row(int tile, int c, const SkinnyParams& p) 
   }
 }
 
-template <typename T, int WAVES, int UNROLL, int MT, int EPI, bool NTL = true>
+template <typename T, int WAVES, int UNROLL, int MT, int EPI, bool NTL = false>
 __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
   using MF = MfmaK32<T>;
   using frag8 = typename MF::frag8;
@@ -185,7 +185,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
     if (s < nsteps) compute(wa, s * STEP);
   }
   for (int k = nsteps * STEP; k < kw; k += 32) {  // tail (K not a multiple of the stage)
-    const frag8 wf = __builtin_nontemporal_load(reinterpret_cast<const frag8*>(wp + k));
+    const frag8 wf = *reinterpret_cast<const frag8*>(wp + k);
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       const frag8 xf = xv[t] ? *reinterpret_cast<const frag8*>(xp[t] + k) : frag8{};
@@ -319,13 +319,25 @@ static void launch_t(int dtype, dim3 grid, hipStream_t st, const SkinnyParams& p
 template <int EPI>
 static void launch_epi(int dtype, int mt, int waves, dim3 grid, hipStream_t st,
                        const SkinnyParams& p) {
-  if (waves == 8) {
-    if (mt == 1) launch_t<8, 4, 1, EPI>(dtype, grid, st, p);
-    else launch_t<8, 4, 2, EPI>(dtype, grid, st, p);
+  // (waves, unroll) picked from the on-device sweep (profiles/r1_microbench_*):
+  // 8 waves x 2-deep stages for the small projections, 16 x 2 for gate_up / down / lm_head.
+  if (waves == 16) {
+    if (mt == 1) launch_t<16, 2, 1, EPI>(dtype, grid, st, p);
+    else launch_t<16, 2, 2, EPI>(dtype, grid, st, p);
+  } else if (waves == 8) {
+    if (mt == 1) launch_t<8, 2, 1, EPI>(dtype, grid, st, p);
+    else launch_t<8, 2, 2, EPI>(dtype, grid, st, p);
   } else {
     if (mt == 1) launch_t<4, 4, 1, EPI>(dtype, grid, st, p);
     else launch_t<4, 4, 2, EPI>(dtype, grid, st, p);
   }
+}
+
+// Largest supported wave count <= requested that divides K into 32-wide MFMA steps.
+static int fit_waves(int waves, int K) {
+  if (waves != 4 && waves != 8 && waves != 16) waves = 8;
+  while (waves > 4 && K % (32 * waves) != 0) waves >>= 1;
+  return waves;
 }
 
 __global__ void sample_finalize_kernel(int64_t* out, unsigned long long* keys, int M) {
@@ -350,7 +362,7 @@ static int skinny_checks(int M, int K, int waves) {
 int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual, int M, int N,
                      int K, int64_t x_stride, int64_t y_stride, int64_t res_stride, int waves,
                      int dtype, hipStream_t stream) {
-  if (waves != 4 && waves != 8) waves = 8;
+  waves = fit_waves(waves, K);
   if (skinny_checks(M, K, waves) || N % 16 != 0) return -1;
   SkinnyParams p{};
   p.x = static_cast<const uint16_t*>(x);
@@ -381,7 +393,7 @@ int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x
                         const int* positions, const int* slots, const float* cos_sin, int M,
                         int K, int64_t x_stride, int64_t q_stride, int n_q_heads, int n_kv_heads,
                         int block_size, float eps, int waves, int dtype, hipStream_t stream) {
-  if (waves != 4 && waves != 8) waves = 8;
+  waves = fit_waves(waves, K);
   if (skinny_checks(M, K, waves)) return -1;
   int shift = 0;
   while ((1 << shift) < block_size) ++shift;
@@ -412,7 +424,7 @@ int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x
 int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int K, int inter,
                             int64_t x_stride, int64_t out_stride, float eps, int waves, int dtype,
                             hipStream_t stream) {
-  if (waves != 4 && waves != 8) waves = 8;
+  waves = fit_waves(waves, K);
   if (skinny_checks(M, K, waves) || inter % 8 != 0) return -1;
   SkinnyParams p{};
   p.x = static_cast<const uint16_t*>(x);
@@ -435,7 +447,7 @@ int atta_fused_lm_head_sample(int64_t* tokens, unsigned long long* keys, const v
                               const float* temperature, const int64_t* seeds,
                               const int64_t* steps, int finalize, int waves, int dtype,
                               hipStream_t stream) {
-  if (waves != 4 && waves != 8) waves = 8;
+  waves = fit_waves(waves, K);
   if (skinny_checks(M, K, waves) || N % 16 != 0) return -1;
   SkinnyParams p{};
   p.x = static_cast<const uint16_t*>(x);
@@ -473,13 +485,13 @@ int atta_skinny_variant(void* y, const void* x, const void* w, int M, int N, int
   if (K % (32 * waves_of[variant & 7])) return -1;
   switch (variant) {
     case 0: skinny_kernel<__bf16, 8, 4, 1, EPI_PLAIN, true><<<grid, 512, 0, stream>>>(p); break;
-    case 1: skinny_kernel<__bf16, 8, 8, 1, EPI_PLAIN, true><<<grid, 512, 0, stream>>>(p); break;
-    case 2: skinny_kernel<__bf16, 4, 4, 1, EPI_PLAIN, true><<<grid, 256, 0, stream>>>(p); break;
-    case 3: skinny_kernel<__bf16, 4, 8, 1, EPI_PLAIN, true><<<grid, 256, 0, stream>>>(p); break;
+    case 1: skinny_kernel<__bf16, 8, 8, 1, EPI_PLAIN, false><<<grid, 512, 0, stream>>>(p); break;
+    case 2: skinny_kernel<__bf16, 4, 4, 1, EPI_PLAIN, false><<<grid, 256, 0, stream>>>(p); break;
+    case 3: skinny_kernel<__bf16, 4, 8, 1, EPI_PLAIN, false><<<grid, 256, 0, stream>>>(p); break;
     case 4: skinny_kernel<__bf16, 8, 4, 1, EPI_PLAIN, false><<<grid, 512, 0, stream>>>(p); break;
-    case 5: skinny_kernel<__bf16, 16, 4, 1, EPI_PLAIN, true><<<grid, 1024, 0, stream>>>(p); break;
-    case 6: skinny_kernel<__bf16, 8, 2, 1, EPI_PLAIN, true><<<grid, 512, 0, stream>>>(p); break;
-    case 7: skinny_kernel<__bf16, 16, 2, 1, EPI_PLAIN, true><<<grid, 1024, 0, stream>>>(p); break;
+    case 5: skinny_kernel<__bf16, 16, 4, 1, EPI_PLAIN, false><<<grid, 1024, 0, stream>>>(p); break;
+    case 6: skinny_kernel<__bf16, 8, 2, 1, EPI_PLAIN, false><<<grid, 512, 0, stream>>>(p); break;
+    case 7: skinny_kernel<__bf16, 16, 2, 1, EPI_PLAIN, false><<<grid, 1024, 0, stream>>>(p); break;
     default: return -1;
   }
   return static_cast<int>(hipGetLastError());

@@ -114,6 +114,9 @@ class ServerState:
             m.heartbeat_age.set(max(0.0, time.monotonic() - self.aengine.heartbeat))
 
 
+STATE_KEY = web.AppKey("state", ServerState)
+
+
 def _log_prompt(st: ServerState, source: str, prompt: str):
     if not st.s.log_requests:
         return
@@ -124,7 +127,7 @@ def _log_prompt(st: ServerState, source: str, prompt: str):
 
 
 async def handle_health(request: web.Request) -> web.Response:
-    st: ServerState = request.app["state"]
+    st: ServerState = request.app[STATE_KEY]
     if st.aengine is not None and (not st.aengine.alive or st.aengine.stalled(st.s.watchdog_s)):
         return web.json_response({"status": "unhealthy", "reason": "engine loop stalled"},
                                  status=503)
@@ -132,7 +135,7 @@ async def handle_health(request: web.Request) -> web.Response:
 
 
 async def handle_metrics(request: web.Request) -> web.Response:
-    st: ServerState = request.app["state"]
+    st: ServerState = request.app[STATE_KEY]
     if st.metrics is None:
         return web.json_response({"error": "Metrics disabled"}, status=503)
     st.refresh_gauges()
@@ -140,7 +143,7 @@ async def handle_metrics(request: web.Request) -> web.Response:
 
 
 async def handle_chat(request: web.Request) -> web.Response:
-    st: ServerState = request.app["state"]
+    st: ServerState = request.app[STATE_KEY]
     if st.engine is None or st.aengine is None:
         return web.json_response({"error": "Backend not initialized"}, status=503)
     ctx = otel.extract(dict(request.headers))
@@ -290,7 +293,7 @@ async def handle_chat(request: web.Request) -> web.Response:
 
 def create_app(state: ServerState) -> web.Application:
     app = web.Application(client_max_size=64 * 1024 * 1024)
-    app["state"] = state
+    app[STATE_KEY] = state
     app.router.add_get("/health", handle_health)
     app.router.add_get("/ready", handle_health)
     app.router.add_get("/live", handle_health)

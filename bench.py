@@ -94,6 +94,14 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
 
+    if a.verbose and rank == 0:
+        tm, rt = eng.timing, eng.runner.timing
+        n = max(1, tm["steps"])
+        g = max(1, eng.runner.graph_steps)
+        log(f"host step breakdown over {n} steps: schedule {tm['schedule'] / n * 1e3:.3f} ms, "
+            f"execute {tm['execute'] / n * 1e3:.3f} ms, post {tm['post'] / n * 1e3:.3f} ms; "
+            f"graph steps {eng.runner.graph_steps}: prep {rt['graph_prep'] / g * 1e3:.3f} ms, "
+            f"replay+sync {rt['graph_run'] / g * 1e3:.3f} ms")
     tokens = sum(r.completion_tokens for r in results)
     ttfts = [t for r in results for t in r.ttfts]
     lat = [t for r in results for t in r.latencies]

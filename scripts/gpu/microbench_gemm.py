@@ -18,7 +18,7 @@ from agentic_traffic_testing_amd import ops  # noqa: E402
 
 SHAPES = [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096),
           ("down", 4096, 14336), ("lm_head", 128256, 4096)]
-VARIANTS = {0: "w8u4", 1: "w8u8", 2: "w4u4", 3: "w4u8", 4: "w8u4-plain", 5: "w16u4",
+VARIANTS = {0: "w8u4-nt", 1: "w8u8", 2: "w4u4", 3: "w4u8", 4: "w8u4", 5: "w16u4",
             6: "w8u2", 7: "w16u2"}
 
 

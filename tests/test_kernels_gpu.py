@@ -294,7 +294,7 @@ def test_decode_lm_head_sample(m):
 
 
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (8, 1), (64, 8)])
-@pytest.mark.parametrize("part_tokens", [64, 256])
+@pytest.mark.parametrize("part_tokens", [128, 256, 512])
 def test_attention_decode_v2(hq, hkv, part_tokens):
     torch.manual_seed(11)
     dt, bs = torch.bfloat16, 16
