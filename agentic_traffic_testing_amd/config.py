@@ -157,6 +157,13 @@ class EngineConfig:
     fused_decode: bool = True
     num_kv_blocks: int = 0               # 0 = size from gpu_memory_utilization
     load_format: str = "auto"            # auto | dummy (random init) | safetensors
+    # tensor parallelism: "auto" = RCCL ("nccl") on GPUs, gloo on CPU; "gloo" forces the
+    # host path (e.g. several ranks rehearsing on one GPU); tp_same_device puts every rank
+    # on the first device (single-GPU rehearsal of the TP protocol)
+    tp_backend: str = "auto"
+    tp_same_device: bool = False
+    tp_allreduce: str = "auto"           # auto | rccl | ipc (custom one-shot all-reduce)
+    dist_port: int = 0                   # 0 = pick a free port
 
     def replace(self, **kw) -> "EngineConfig":
         return replace(self, **kw)

@@ -52,6 +52,7 @@ class AsyncEngine:
         self._wake.set()
         if self._thread is not None:
             self._thread.join(timeout=10)
+        self.engine.shutdown()
 
     def stalled(self, threshold_s: float = 60.0) -> bool:
         busy = bool(self._pending) or self.engine.has_unfinished()

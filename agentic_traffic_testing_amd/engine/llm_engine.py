@@ -192,6 +192,9 @@ class LLMEngine:
             "prefix_hits": r.bm.prefix_hits(),
         }
 
+    def shutdown(self):
+        """Release engine resources (TP engines stop their worker ranks)."""
+
     def est_max_concurrency(self) -> float:
         return self.runner.kv_total_tokens / max(1, self.cfg.max_model_len)
 

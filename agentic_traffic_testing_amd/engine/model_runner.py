@@ -12,6 +12,11 @@ One step = one forward over a decode-first ``Batch`` (scheduler.py) followed by 
 * **hipGraphs** - decode-only steps are padded to a bucket (1, 2, 4, 8, ...) and replayed
   from a captured graph that contains the whole forward, the LM head and the sampler, so a
   decode step costs one graph launch instead of ~330 kernel launches.
+* **Tensor parallelism** - rank 0 owns scheduler + block manager; every step it packs the
+  same int32 metadata it uploads into a step message (header + payload) and publishes it
+  on a shared-memory channel (runtime/csrc/shm_channel.cpp).  TP worker ranks
+  (``serve_worker``) replay exactly the same kernel / collective sequence from it, graph
+  captures included, so the RCCL all-reduces line up.
 """
 from __future__ import annotations
 
@@ -89,17 +94,25 @@ class MetaLayout:
                 host[o:o + n][:a.size] = a.reshape(-1)
 
 
+# step-message header (int32 words) shared by rank 0 and the TP workers
+HDR_WORDS = 12
+OP_STEP, OP_CAPTURE, OP_STOP = 1, 2, 3
+
+
 class ModelRunner:
     def __init__(self, cfg: EngineConfig, model_cfg: ModelConfig, device: str = "cuda",
-                 tp_rank: int = 0, tp_size: int = 1, tp_group=None, weights_dir=None):
+                 comm=None, weights_dir=None):
         self.cfg = cfg
         self.mcfg = model_cfg
         self.device = torch.device(device)
         self.is_cuda = self.device.type == "cuda"
         self.dtype = torch_dtype(cfg.dtype)
+        self.comm = comm
+        tp_rank, tp_size = (comm.rank, comm.size) if comm is not None else (0, 1)
         self.tp_rank, self.tp_size = tp_rank, tp_size
+        self.publisher = None     # rank 0 of a TP group: ShmChannel to the workers
         t0 = time.perf_counter()
-        self.model = LlamaModel(model_cfg, self.dtype, self.device, tp_rank, tp_size, tp_group)
+        self.model = LlamaModel(model_cfg, self.dtype, self.device, tp_rank, tp_size, comm)
         if weights_dir and cfg.load_format != "dummy":
             self.model.load_safetensors(weights_dir)
         else:
@@ -111,6 +124,8 @@ class ModelRunner:
         self.max_parts = max(1, math.ceil(cfg.max_model_len / self.part_tokens))
         self.tile_tokens = ops.PREFILL_TILE_TOKENS.get(self.model.g, 16)
         self.graph_sizes = sorted(b for b in cfg.graph_batch_sizes)
+        if comm is not None and comm.size > 1 and comm.is_gloo:
+            self.graph_sizes = []  # gloo collectives are host-side: nothing to capture
         cap = next((b for b in self.graph_sizes if b >= cfg.max_num_seqs), cfg.max_num_seqs)
         self.graph_sizes = [b for b in self.graph_sizes if b <= cap]
         self.max_seqs = max(cfg.max_num_seqs, self.graph_sizes[-1] if self.graph_sizes else 1)
@@ -137,8 +152,10 @@ class ModelRunner:
             "q": torch.empty(self.max_seqs, self.model.n_heads, 128, dtype=dt, device=dev),
             "attn": torch.empty(self.max_seqs, self.model.n_heads, 128, dtype=dt, device=dev),
             "act": torch.empty(self.max_seqs, self.model.inter, dtype=dt, device=dev),
-            "keys": torch.zeros(self.max_seqs, dtype=torch.int64, device=dev),
+            "keys": torch.zeros(self.max_seqs * (self.model.vocab_shard // 16 + 1),
+                                dtype=torch.int64, device=dev),
             "tokens": torch.zeros(self.max_seqs, dtype=torch.int64, device=dev),
+            "tp_keys": torch.zeros(self.max_seqs, dtype=torch.int64, device=dev),
             "counters": torch.zeros(self.max_seqs * nkv, dtype=torch.int32, device=dev),
             "part_out": self.part_out, "part_lse": self.part_lse,
             "max_parts": self.max_parts, "part_tokens": self.part_tokens,
@@ -172,6 +189,8 @@ class ModelRunner:
         else:
             nb = int(os.environ.get("ATTA_CPU_KV_BLOCKS", "256"))
         nb = max(nb, 2 * self.bt_width)
+        if self.comm is not None:  # TP ranks must agree on the page count
+            nb = self.comm.min_int(nb, self.device)
         self.num_blocks = nb
         shape_k = (L, nb, m.n_kv_heads, self.block_size, m.head_dim)
         shape_v = (L, nb, m.n_kv_heads, m.head_dim, self.block_size)
@@ -213,12 +232,10 @@ class ModelRunner:
         arrays.update(input_ids=input_ids, temperature=temps, seeds=seeds, steps=steps)
         return lay, arrays
 
-    def _upload(self, lay: MetaLayout, arrays: dict, dev_buf=None):
+    def _pack(self, lay: MetaLayout, arrays: dict) -> np.ndarray:
         host = self.meta_host_np[:lay.size]
         lay.pack(host, arrays)
-        dev = self.meta_dev[:lay.size] if dev_buf is None else dev_buf
-        dev.copy_(self.meta_host[:lay.size], non_blocking=True)
-        return lay.views(dev)
+        return host
 
     def _meta(self, v: dict, num_decode: int, num_tiles: int) -> AttnMeta:
         return AttnMeta(positions=v["positions"], slot_mapping=v["slot_mapping"],
@@ -249,33 +266,86 @@ class ModelRunner:
         self.steps += 1
         special = any(s.sampling.top_p < 1.0 or s.sampling.top_k > 0 for s in batch.seqs)
         decode_only = batch.num_decode == n
+        bucket = 0
         if (self.is_cuda and self.cfg.use_graphs and decode_only and not special
                 and self.graph_sizes and n <= self.graph_sizes[-1]):
             bucket = next(b for b in self.graph_sizes if b >= n)
             if bucket not in self.graphs:
                 self.capture(bucket)
-            io = self.graph_io[bucket]
-            t0 = time.perf_counter()
+        t0 = time.perf_counter()
+        if bucket:
             lay, arrays = self._prepare(batch, pad_seqs=bucket, tiles=False)
-            assert lay.size == io["layout"].size
-            self._upload(lay, arrays, io["dev"])
-            t1 = time.perf_counter()
-            self.graphs[bucket].replay()
-            self.graph_steps += 1
-            out = io["out"][:n].cpu().numpy()
+            assert lay.size == self.graph_io[bucket]["layout"].size
+            num_parts = self.max_parts
+        else:
+            lay, arrays = self._prepare(batch)
+            max_kv = int(arrays["seq_kvlen"][:batch.num_decode].max()) if batch.num_decode else 0
+            num_parts = max(1, math.ceil(max_kv / self.part_tokens))
+        host = self._pack(lay, arrays)
+        hdr = np.array([OP_STEP, lay.T, lay.S, lay.W, lay.NT, batch.num_decode, num_parts,
+                        bucket, int(special), n, lay.size, 0], dtype=np.int32)
+        if self.publisher is not None:
+            self.publisher.publish(np.concatenate([hdr, host]))
+        sampler = self._special_sampler(batch) if special else None
+        t1 = time.perf_counter()
+        toks = self._run(hdr, sampler)
+        out = toks[:n].cpu().numpy()
+        if bucket:
             self.timing["graph_prep"] += t1 - t0
             self.timing["graph_run"] += time.perf_counter() - t1
-            return out
-        lay, arrays = self._prepare(batch)
-        v = self._upload(lay, arrays)
-        md = self._meta(v, batch.num_decode, lay.NT)
-        max_kv = int(arrays["seq_kvlen"][:batch.num_decode].max()) if batch.num_decode else 0
-        num_parts = max(1, math.ceil(max_kv / self.part_tokens))
-        sampler = None
-        if special:
-            sampler = self._special_sampler(batch)
-        toks = self._forward_sample(v, md, num_parts, sampler)
-        return toks.cpu().numpy()
+        return out
+
+    def _run(self, hdr, sampler=None, worker: bool = False):
+        """Execute one step from its header; the packed metadata is in ``meta_host``."""
+        T, S, W, NT, num_decode, num_parts, bucket, special, n, size = (int(x) for x in hdr[1:11])
+        if bucket:
+            io = self.graph_io[bucket]
+            io["dev"].copy_(self.meta_host[:size], non_blocking=True)
+            self.graphs[bucket].replay()
+            self.graph_steps += 1
+            return io["out"]
+        lay = MetaLayout(T, S, W, NT)
+        dev = self.meta_dev[:size]
+        dev.copy_(self.meta_host[:size], non_blocking=True)
+        v = lay.views(dev)
+        md = self._meta(v, num_decode, NT)
+        if special and worker:
+            # rank 0 samples (top-p / top-k); workers only join the logits all-gather
+            sampler = _discard_sampler
+        return self._forward_sample(v, md, num_parts, sampler)
+
+    # -- TP worker side ------------------------------------------------------------------
+    def serve_worker(self, channel, reader: int) -> None:
+        """TP rank > 0: replay rank 0's steps until it publishes OP_STOP / closes."""
+        last = 0
+        while True:
+            msg = channel.receive(reader, last, -1.0)
+            if msg is None:
+                return
+            last, data = msg
+            hdr = data[:HDR_WORDS]
+            op = int(hdr[0])
+            if op == OP_STOP:
+                return
+            if op == OP_CAPTURE:
+                self.capture(int(hdr[1]))
+                continue
+            size = int(hdr[10])
+            self.meta_host_np[:size] = data[HDR_WORDS:HDR_WORDS + size]
+            self._run(hdr, worker=True)
+            self.steps += 1
+            if self.is_cuda:
+                # meta_host is reused by the next message: drain this step's H2D copy first
+                torch.cuda.current_stream(self.device).synchronize()
+
+    def stop_workers(self):
+        if self.publisher is not None:
+            hdr = np.zeros(HDR_WORDS, dtype=np.int32)
+            hdr[0] = OP_STOP
+            try:
+                self.publisher.publish(hdr, 30.0)
+            finally:
+                self.publisher.close()
 
     def _special_sampler(self, batch: Batch):
         params = [s.sampling for s in batch.seqs]
@@ -310,6 +380,10 @@ class ModelRunner:
     # ------------------------------------------------------------------------------------
     def capture(self, bucket: int):
         """Capture a decode step for `bucket` sequences into a hipGraph."""
+        if self.publisher is not None:
+            hdr = np.zeros(HDR_WORDS, dtype=np.int32)
+            hdr[0], hdr[1] = OP_CAPTURE, bucket
+            self.publisher.publish(hdr)
         lay = MetaLayout(bucket, bucket, self.bt_width, 0)
         dev = torch.zeros(lay.size, dtype=torch.int32, device=self.device)
         v = lay.views(dev)
@@ -345,4 +419,8 @@ class ModelRunner:
         self.bm.reset_prefix_cache()
 
 
-__all__ = ["ModelRunner", "MetaLayout", "ref"]
+def _discard_sampler(logits):
+    return None
+
+
+__all__ = ["ModelRunner", "MetaLayout", "ref", "HDR_WORDS", "OP_STEP", "OP_CAPTURE", "OP_STOP"]

@@ -10,7 +10,8 @@ This is the model vLLM executes inside ``AsyncLLMEngine`` for the reference
   variants), SiLU-mul, sampler;
 * tensor parallelism is Megatron-style: qkv / gate_up column-parallel, o / down row-parallel
   with one all-reduce each (``parallel.comm``); the embedding is replicated and the LM head
-  is vocab-parallel with an all-gather of the [B, V/tp] logits;
+  is vocab-parallel: the fused decode sampler reduces each shard to one packed key per row
+  and an int64 MAX all-reduce picks the winner (prefill all-gathers the [B, V/tp] logits);
 * weights are either seeded random-init (benchmarks: no network, gated checkpoints) or
   loaded from HF safetensors.
 """
@@ -29,7 +30,8 @@ from ..config import ModelConfig
 from ..ops import reference as ref
 
 DTYPES = {"bfloat16": torch.bfloat16, "bf16": torch.bfloat16, "float16": torch.float16,
-          "fp16": torch.float16, "half": torch.float16, "auto": torch.bfloat16}
+          "fp16": torch.float16, "half": torch.float16, "auto": torch.bfloat16,
+          "float32": torch.float32, "fp32": torch.float32}  # fp32: CPU reference runs only
 
 
 def torch_dtype(name: str) -> torch.dtype:
@@ -64,6 +66,7 @@ class LayerWeights:
 class LlamaModel:
     def __init__(self, cfg: ModelConfig, dtype=torch.bfloat16, device="cuda", tp_rank: int = 0,
                  tp_size: int = 1, tp_group=None):
+        # tp_group: parallel.comm.TPComm (required when tp_size > 1)
         self.cfg = cfg
         self.dtype = dtype
         self.device = torch.device(device)
@@ -219,9 +222,7 @@ class LlamaModel:
 
     def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         if self.tp_size > 1:
-            from ..parallel import comm
-
-            comm.tp_all_reduce(x, self.tp_group)
+            self.tp_group.all_reduce(x)
         return x
 
     def forward(self, input_ids: torch.Tensor, md: AttnMeta, k_caches, v_caches,
@@ -299,16 +300,19 @@ class LlamaModel:
         if self.tp_size == 1:
             return ops.decode_lm_head_sample(residual, self.lm_head, eps, temperature, seeds,
                                              steps, ws["keys"], tokens=ws["tokens"][:B])
-        x = ops.rms_norm(residual, self.norm, eps)
-        logits = self.compute_logits(x)
-        return ops.sample(logits, temperature, seeds, steps, out=ws["tokens"][:B])
+        # TP: each rank samples its vocab shard down to one packed key per row (global ids,
+        # so the Gumbel noise equals TP=1's); one int64 MAX all-reduce picks the winner
+        keys = ops.decode_lm_head_sample(residual, self.lm_head, eps, temperature, seeds,
+                                         steps, ws["keys"], tokens=ws["tp_keys"][:B],
+                                         finalize="key",
+                                         vocab_offset=self.tp_rank * self.vocab_shard)
+        self.tp_group.all_reduce_max(keys)
+        return ops.key_to_token(keys)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
         logits = ops.linear(hidden, self.lm_head)
         if self.tp_size > 1:
-            from ..parallel import comm
-
-            logits = comm.tp_all_gather_last(logits, self.tp_group)
+            logits = self.tp_group.all_gather_last(logits)
         return logits
 
 

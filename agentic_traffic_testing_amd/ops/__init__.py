@@ -222,18 +222,33 @@ def decode_gate_up_silu(x, w, eps, out=None):
 
 
 def decode_lm_head_sample(x, w, eps, temperature, seeds, steps, keys, tokens=None,
-                          finalize=True):
+                          finalize=True, vocab_offset=0):
     """Final RMSNorm -> LM head -> greedy / Gumbel-max sample without materialising logits.
-    ``keys`` (int64 [M], zero-initialised once) holds packed (value, index) maxima."""
+    ``keys`` (int64, >= M * vocab/16 entries) is scratch for the per-tile packed
+    (value, index) maxima; no initialisation is needed.
+
+    ``finalize``: True -> ``tokens`` gets token ids; ``"key"`` -> ``tokens`` gets each row's
+    signed-orderable packed key (TP: MAX all-reduce them, then ``key_to_token``); False ->
+    partials only.  ``vocab_offset`` is this shard's first vocab id."""
     if tokens is None:
         tokens = torch.empty(x.shape[0], dtype=torch.long, device=x.device)
     if not x.is_cuda:
         n = ref.rms_norm(x, torch.ones(x.shape[1], dtype=x.dtype), eps)
-        tokens.copy_(ref.sample(torch.nn.functional.linear(n, w), temperature, seeds, steps))
+        logits = torch.nn.functional.linear(n, w)
+        if finalize == "key":
+            tokens.copy_(ref.sample_keys(logits, temperature, seeds, steps, vocab_offset))
+        else:
+            tokens.copy_(ref.sample(logits, temperature, seeds, steps, vocab_offset))
         return tokens
-    _native().fused_lm_head_sample(tokens, keys, x, w, eps, temperature, seeds, steps, finalize,
-                                   WAVES_LARGE)
+    mode = 2 if finalize == "key" else (1 if finalize else 0)
+    _native().fused_lm_head_sample(tokens, keys, x, w, eps, temperature, seeds, steps, mode,
+                                   vocab_offset, WAVES_LARGE)
     return tokens
+
+
+def key_to_token(keys: torch.Tensor) -> torch.Tensor:
+    """Decode signed-orderable packed sampler keys (``finalize="key"``) to token ids."""
+    return 0xFFFFFFFF - (keys & 0xFFFFFFFF)
 
 
 def attention_decode_v2(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, scale,

@@ -217,30 +217,34 @@ void fused_gate_up_silu(at::Tensor out, const at::Tensor& x, const at::Tensor& w
 
 void fused_lm_head_sample(at::Tensor tokens, at::Tensor keys, const at::Tensor& x,
                           const at::Tensor& w, double eps, const at::Tensor& temperature,
-                          const at::Tensor& seeds, const at::Tensor& steps, bool finalize,
-                          int64_t waves) {
+                          const at::Tensor& seeds, const at::Tensor& steps, int64_t finalize,
+                          int64_t vocab_offset, int64_t waves) {
+  TORCH_CHECK(finalize >= 0 && finalize <= 2, "fused_lm_head_sample: finalize mode 0/1/2");
   check_skinny(x, w, "fused_lm_head_sample");
   TORCH_CHECK(tokens.scalar_type() == at::kLong && keys.scalar_type() == at::kLong &&
                   seeds.scalar_type() == at::kLong && steps.scalar_type() == at::kLong &&
                   temperature.scalar_type() == at::kFloat,
               "fused_lm_head_sample: dtypes");
-  TORCH_CHECK(keys.numel() >= x.size(0) && tokens.numel() >= x.size(0), "fused_lm_head_sample: sizes");
+  TORCH_CHECK(keys.numel() >= x.size(0) * (w.size(0) / 16) && tokens.numel() >= x.size(0),
+              "fused_lm_head_sample: keys needs M * (vocab / 16) entries");
   const at::DeviceGuard g(x.device());
   check_rc(atta_fused_lm_head_sample(
                tokens.data_ptr<int64_t>(),
                reinterpret_cast<unsigned long long*>(keys.data_ptr<int64_t>()), x.data_ptr(),
                w.data_ptr(), x.size(0), w.size(0), x.size(1), x.stride(0), static_cast<float>(eps),
                temperature.data_ptr<float>(), seeds.data_ptr<int64_t>(), steps.data_ptr<int64_t>(),
-               finalize ? 1 : 0, waves, dtype_code(x), cur_stream()),
+               static_cast<int>(finalize), static_cast<int>(vocab_offset), waves, dtype_code(x),
+               cur_stream()),
            "fused_lm_head_sample");
 }
 
-void sample_finalize(at::Tensor tokens, at::Tensor keys) {
+void sample_finalize(at::Tensor tokens, const at::Tensor& keys, int64_t n_tiles) {
   check_dev(keys, "keys");
+  TORCH_CHECK(n_tiles > 0 && keys.numel() >= tokens.numel() * n_tiles, "sample_finalize: sizes");
   const at::DeviceGuard g(keys.device());
   check_rc(atta_sample_finalize(tokens.data_ptr<int64_t>(),
-                                reinterpret_cast<unsigned long long*>(keys.data_ptr<int64_t>()),
-                                keys.numel(), cur_stream()),
+                                reinterpret_cast<const unsigned long long*>(keys.data_ptr<int64_t>()),
+                                tokens.numel(), n_tiles, cur_stream()),
            "sample_finalize");
 }
 
@@ -297,8 +301,9 @@ TORCH_LIBRARY(atta, m) {
   m.def("fused_gate_up_silu(Tensor(a!) out, Tensor x, Tensor w, float eps, int waves) -> ()");
   m.def(
       "fused_lm_head_sample(Tensor(a!) tokens, Tensor(b!) keys, Tensor x, Tensor w, float eps, "
-      "Tensor temperature, Tensor seeds, Tensor steps, bool finalize, int waves) -> ()");
-  m.def("sample_finalize(Tensor(a!) tokens, Tensor(b!) keys) -> ()");
+      "Tensor temperature, Tensor seeds, Tensor steps, int finalize, int vocab_offset, "
+      "int waves) -> ()");
+  m.def("sample_finalize(Tensor(a!) tokens, Tensor keys, int n_tiles) -> ()");
   m.def("skinny_gemm(Tensor(a!) y, Tensor x, Tensor w, Tensor? residual, int waves) -> ()");
   m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rms_norm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");

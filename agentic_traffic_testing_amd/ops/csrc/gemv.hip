@@ -22,8 +22,9 @@
 //       PLAIN   y = acc                      RESADD  r += acc (residual stream, in place)
 //       QKVROPE q/k rotated (RoPE) -> q buffer / paged K cache, v -> transposed V cache
 //       SILU    out[:, j] = silu(gate_j) * up_j
-//       SAMPLE  logits -> greedy / Gumbel-max key -> atomicMax per row (sampler fused
-//               into the LM head; `sample_finalize` turns keys into token ids)
+//       SAMPLE  logits -> greedy / Gumbel-max key -> one partial max per (row, tile)
+//               (sampler fused into the LM head; `sample_finalize` reduces a row's
+//               partials to its token id with one workgroup per row)
 #include "common.h"
 #include "kernels.h"
 
@@ -83,7 +84,9 @@ struct SkinnyParams {
   // SILU
   int inter;
   // SAMPLE
-  unsigned long long* keys;
+  unsigned long long* keys;  // [M, key_stride] per-tile partial maxima
+  int key_stride;
+  int vocab_offset;          // first vocab id of this TP rank's LM-head shard
   const float* temperature;
   const int64_t* seeds;
   const int64_t* steps;
@@ -290,7 +293,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
         const float sc = norm ? inv_rms[m] : 1.f;
         float v = to_f32<T>(from_f32<T>(red[0][m][n] * sc));  // bf16 logits, as F.linear
         const float t = p.temperature[m];
-        const int idx = tile * 16 + n;
+        const int idx = p.vocab_offset + tile * 16 + n;  // global id: TP == TP1 noise
         if (t > 1e-5f)
           v = v / t + gumbel_noise(static_cast<uint64_t>(p.seeds[m]),
                                    static_cast<uint64_t>(p.steps[m]), static_cast<uint32_t>(idx));
@@ -303,7 +306,8 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
         const unsigned long long other = __shfl_xor(key, o, kWave);
         key = other > key ? other : key;
       }
-      if (n == 0 && m < p.M) atomicMax(p.keys + m, key);
+      // one plain store per (row, tile): no same-address atomics across the ~8k tiles
+      if (n == 0 && m < p.M) p.keys[static_cast<int64_t>(m) * p.key_stride + tile] = key;
     }
   }
 }
@@ -340,15 +344,51 @@ static int fit_waves(int waves, int K) {
   return waves;
 }
 
-__global__ void sample_finalize_kernel(int64_t* out, unsigned long long* keys, int M) {
-  const int m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m < M) {
-    const unsigned long long k = keys[m];
-    out[m] = static_cast<int64_t>(0xFFFFFFFFu - static_cast<unsigned>(k & 0xFFFFFFFFull));
-    keys[m] = 0ull;  // re-arm for the next launch (keys start zeroed at allocation)
+// One workgroup per row reduces the row's per-tile partial keys to the winning token.
+// 1024 threads x 8 independent loads in flight cover the 8016 partials of a 128256 vocab
+// in one memory round trip.
+// KEY_OUT writes the row's packed key with the sign bit flipped (signed-int64 orderable) so
+// TP ranks can combine their vocab shards with one int64 MAX all-reduce.
+constexpr int kFinThreads = 1024;
+template <bool KEY_OUT>
+__global__ void __launch_bounds__(kFinThreads) sample_finalize_kernel(
+    int64_t* out, const unsigned long long* keys, int n_tiles) {
+  __shared__ unsigned long long red[kFinThreads / kWave];
+  const int m = blockIdx.x;
+  const unsigned long long* row = keys + static_cast<int64_t>(m) * n_tiles;
+  unsigned long long best = 0ull;
+  for (int base = 0; base < n_tiles; base += 8 * kFinThreads) {
+    unsigned long long k[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = base + j * kFinThreads + threadIdx.x;
+      k[j] = i < n_tiles ? row[i] : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) best = k[j] > best ? k[j] : best;
+  }
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const unsigned long long other = __shfl_xor(best, o, kWave);
+    best = other > best ? other : best;
+  }
+  if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = best;
+  __syncthreads();
+  if (threadIdx.x < kWave) {
+    best = threadIdx.x < kFinThreads / kWave ? red[threadIdx.x] : 0ull;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const unsigned long long other = __shfl_xor(best, o, kWave);
+      best = other > best ? other : best;
+    }
+    if (threadIdx.x == 0) {
+      if constexpr (KEY_OUT)
+        out[m] = static_cast<int64_t>(best ^ 0x8000000000000000ull);
+      else
+        out[m] = static_cast<int64_t>(0xFFFFFFFFu - static_cast<unsigned>(best & 0xFFFFFFFFull));
+    }
   }
 }
-
 }  // namespace atta
 
 using namespace atta;
@@ -445,8 +485,8 @@ int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int 
 int atta_fused_lm_head_sample(int64_t* tokens, unsigned long long* keys, const void* x,
                               const void* w, int M, int N, int K, int64_t x_stride, float eps,
                               const float* temperature, const int64_t* seeds,
-                              const int64_t* steps, int finalize, int waves, int dtype,
-                              hipStream_t stream) {
+                              const int64_t* steps, int finalize, int vocab_offset,
+                              int waves, int dtype, hipStream_t stream) {
   waves = fit_waves(waves, K);
   if (skinny_checks(M, K, waves) || N % 16 != 0) return -1;
   SkinnyParams p{};
@@ -458,12 +498,17 @@ int atta_fused_lm_head_sample(int64_t* tokens, unsigned long long* keys, const v
   p.K = K;
   p.eps = eps;
   p.keys = keys;
+  p.key_stride = N / 16;
+  p.vocab_offset = vocab_offset;
   p.temperature = temperature;
   p.seeds = seeds;
   p.steps = steps;
   dim3 grid(N / 16);
   launch_epi<EPI_SAMPLE>(dtype, M <= 16 ? 1 : 2, waves, grid, stream, p);
-  if (finalize) sample_finalize_kernel<<<(M + 63) / 64, 64, 0, stream>>>(tokens, keys, M);
+  if (finalize == 1)
+    sample_finalize_kernel<false><<<M, kFinThreads, 0, stream>>>(tokens, keys, N / 16);
+  else if (finalize == 2)
+    sample_finalize_kernel<true><<<M, kFinThreads, 0, stream>>>(tokens, keys, N / 16);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -497,7 +542,9 @@ int atta_skinny_variant(void* y, const void* x, const void* w, int M, int N, int
   return static_cast<int>(hipGetLastError());
 }
 
-int atta_sample_finalize(int64_t* tokens, unsigned long long* keys, int M, hipStream_t stream) {
-  sample_finalize_kernel<<<(M + 63) / 64, 64, 0, stream>>>(tokens, keys, M);
+int atta_sample_finalize(int64_t* tokens, const unsigned long long* keys, int M, int n_tiles,
+                         hipStream_t stream) {
+  if (M <= 0 || n_tiles <= 0) return 0;
+  sample_finalize_kernel<false><<<M, kFinThreads, 0, stream>>>(tokens, keys, n_tiles);
   return static_cast<int>(hipGetLastError());
 }

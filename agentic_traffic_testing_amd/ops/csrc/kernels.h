@@ -52,10 +52,11 @@ int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int 
 int atta_fused_lm_head_sample(int64_t* tokens, unsigned long long* keys, const void* x,
                               const void* w, int M, int N, int K, int64_t x_stride, float eps,
                               const float* temperature, const int64_t* seeds,
-                              const int64_t* steps, int finalize, int waves, int dtype,
-                              hipStream_t stream);
+                              const int64_t* steps, int finalize, int vocab_offset,
+                              int waves, int dtype, hipStream_t stream);
 
-int atta_sample_finalize(int64_t* tokens, unsigned long long* keys, int M, hipStream_t stream);
+int atta_sample_finalize(int64_t* tokens, const unsigned long long* keys, int M, int n_tiles,
+                         hipStream_t stream);
 
 int atta_attention_decode_v2(void* out, float* part_out, float* part_lse, int* counters,
                              const void* q, const void* k_cache, const void* v_cache,

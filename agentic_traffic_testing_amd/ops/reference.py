@@ -113,20 +113,45 @@ def paged_attention(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, sc
     return out
 
 
+def _sample_scores(lf: torch.Tensor, r: int, temperature, seeds, steps, vocab_offset: int):
+    t = float(temperature[r])
+    if not t > 1e-5:
+        return lf[r]
+    idx = torch.arange(vocab_offset, vocab_offset + lf.shape[1], dtype=torch.int64)
+    return lf[r] / t + gumbel_noise(int(seeds[r]), int(steps[r]), idx).to(lf.device)
+
+
 def sample(logits: torch.Tensor, temperature: torch.Tensor, seeds: torch.Tensor,
-           steps: torch.Tensor) -> torch.Tensor:
-    """Greedy for temperature<=1e-5, else Gumbel-max with the kernel's counter-based RNG."""
+           steps: torch.Tensor, vocab_offset: int = 0) -> torch.Tensor:
+    """Greedy for temperature<=1e-5, else Gumbel-max with the kernel's counter-based RNG.
+    ``vocab_offset`` = global id of column 0 (TP vocab shard); returned ids are global."""
     lf = logits.float()
     out = torch.empty(lf.shape[0], dtype=torch.long, device=logits.device)
-    vocab = lf.shape[1]
-    idx = torch.arange(vocab, dtype=torch.int64)
     for r in range(lf.shape[0]):
-        t = float(temperature[r])
-        if not t > 1e-5:
-            out[r] = int(torch.argmax(lf[r]))
-            continue
-        g = gumbel_noise(int(seeds[r]), int(steps[r]), idx).to(lf.device)
-        out[r] = int(torch.argmax(lf[r] / t + g))
+        sc = _sample_scores(lf, r, temperature, seeds, steps, vocab_offset)
+        out[r] = int(torch.argmax(sc)) + vocab_offset
+    return out
+
+
+def _ordered_bits(v: float) -> int:
+    import struct
+
+    b = struct.unpack("<I", struct.pack("<f", v))[0]
+    return (~b & 0xFFFFFFFF) if b & 0x80000000 else (b | 0x80000000)
+
+
+def sample_keys(logits: torch.Tensor, temperature: torch.Tensor, seeds: torch.Tensor,
+                steps: torch.Tensor, vocab_offset: int = 0) -> torch.Tensor:
+    """Signed-orderable packed (score, -id) keys of each row's winner, as the kernel's
+    ``finalize="key"`` mode emits them: MAX over TP shards picks the global winner."""
+    lf = logits.float()
+    out = torch.empty(lf.shape[0], dtype=torch.long, device=logits.device)
+    for r in range(lf.shape[0]):
+        sc = _sample_scores(lf, r, temperature, seeds, steps, vocab_offset)
+        j = int(torch.argmax(sc))
+        key = (_ordered_bits(float(sc[j])) << 32) | (0xFFFFFFFF - (j + vocab_offset))
+        key ^= 1 << 63
+        out[r] = key - (1 << 64) if key >= (1 << 63) else key
     return out
 
 

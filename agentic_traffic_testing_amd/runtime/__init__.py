@@ -1,4 +1,5 @@
-"""Native serving runtime (C++ via pybind11): block manager + batch builder.
+"""Native serving runtime (C++ via pybind11): block manager + batch builder, and the
+shared-memory step channel used by tensor-parallel ranks.
 
 The extension is built in-tree by ``ops/build.py``; importing this package builds it on
 first use if the shared object is missing.
@@ -23,5 +24,6 @@ def _load():
 
 _rt = _load()
 BlockManager = _rt.BlockManager
+ShmChannel = _rt.ShmChannel
 
-__all__ = ["BlockManager"]
+__all__ = ["BlockManager", "ShmChannel"]

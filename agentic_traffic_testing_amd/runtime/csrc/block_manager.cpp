@@ -338,8 +338,7 @@ class BlockManager {
 
 }  // namespace
 
-PYBIND11_MODULE(_atta_runtime, m) {
-  m.doc() = "Native paged-KV block manager + batch builder (agentic_traffic_testing_amd)";
+void register_block_manager(py::module_& m) {
   py::class_<BlockManager>(m, "BlockManager")
       .def(py::init<int, int, bool>(), py::arg("num_blocks"), py::arg("block_size"),
            py::arg("prefix_caching") = true)

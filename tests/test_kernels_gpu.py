@@ -274,12 +274,12 @@ def test_decode_lm_head_sample(m):
     dt, V, H = torch.bfloat16, 32768, 1024
     x = torch.randn(m, H, dtype=dt, device="cuda")
     w = torch.randn(V, H, dtype=dt, device="cuda") * 0.05
-    keys = torch.zeros(32, dtype=torch.int64, device="cuda")
+    keys = torch.full((32 * V // 16,), -1, dtype=torch.int64, device="cuda")  # garbage scratch
     temp = torch.zeros(m, device="cuda")
     seeds = torch.arange(m, dtype=torch.int64, device="cuda")
     steps = torch.zeros(m, dtype=torch.int64, device="cuda")
     logits = torch.nn.functional.linear(_norm_ref(x), w).float()
-    for _ in range(3):  # keys must re-arm between launches
+    for _ in range(3):  # repeated launches reuse the scratch
         got = ops.decode_lm_head_sample(x, w, 1e-5, temp, seeds, steps, keys)
         top2 = torch.topk(logits, 2, dim=-1)
         for r in range(m):
@@ -287,10 +287,39 @@ def test_decode_lm_head_sample(m):
             # exact argmax unless the top-2 are within bf16 rounding of each other
             assert g == int(top2.indices[r, 0]) or \
                 float(top2.values[r, 0] - logits[r, g]) < 0.05
-    assert bool((keys == 0).all())
     temp.fill_(0.8)
     toks = ops.decode_lm_head_sample(x, w, 1e-5, temp, seeds, steps, keys)
     assert bool(((toks >= 0) & (toks < V)).all())
+
+
+@pytest.mark.parametrize("m", [1, 7])
+def test_decode_lm_head_sample_vocab_parallel(m):
+    """TP path: two vocab shards emit signed-orderable keys (global ids for the noise);
+    their MAX must equal sampling over the full vocabulary."""
+    torch.manual_seed(12)
+    dt, V, H = torch.bfloat16, 8192, 1024
+    x = torch.randn(m, H, dtype=dt, device="cuda")
+    w = torch.randn(V, H, dtype=dt, device="cuda") * 0.05
+    keys = torch.empty(m * V // 16, dtype=torch.int64, device="cuda")
+    temp = torch.full((m,), 0.7, device="cuda")
+    temp[0] = 0.0
+    seeds = torch.arange(m, dtype=torch.int64, device="cuda") + 5
+    steps = torch.full((m,), 3, dtype=torch.int64, device="cuda")
+    full = ops.decode_lm_head_sample(x, w, 1e-5, temp, seeds, steps, keys).clone()
+    shard = V // 2
+    k0 = ops.decode_lm_head_sample(x, w[:shard].contiguous(), 1e-5, temp, seeds, steps, keys,
+                                   finalize="key", vocab_offset=0).clone()
+    k1 = ops.decode_lm_head_sample(x, w[shard:].contiguous(), 1e-5, temp, seeds, steps, keys,
+                                   finalize="key", vocab_offset=shard).clone()
+    got = ops.key_to_token(torch.maximum(k0, k1))
+    assert got.tolist() == full.tolist()
+    # keys agree with the fp32 reference's packing on the greedy row
+    logits = torch.nn.functional.linear(_norm_ref(x), w).float().cpu()
+    ref_keys = ref.sample_keys(logits[:1, shard:], temp[:1].cpu(), seeds[:1].cpu(),
+                               steps[:1].cpu(), vocab_offset=shard)
+    assert int(ops.key_to_token(ref_keys)[0]) == int(ops.key_to_token(k1[:1])[0]) or \
+        abs(float(logits[0, int(ops.key_to_token(k1[:1])[0])]) -
+            float(logits[0, int(ops.key_to_token(ref_keys)[0])])) < 0.05
 
 
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (8, 1), (64, 8)])
