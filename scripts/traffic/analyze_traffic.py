@@ -1,0 +1,10 @@
+#!/usr/bin/env python3
+"""CLI: pcap + telemetry analyzer (agentic_traffic_testing_amd.observability.traffic_analysis)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from agentic_traffic_testing_amd.observability.traffic_analysis import main  # noqa: E402
+
+if __name__ == "__main__":
+    sys.exit(main())
