@@ -122,6 +122,13 @@ class ModelRunner:
         self.bt_width = math.ceil(cfg.max_model_len / cfg.block_size)
         self.part_tokens = cfg.decode_partition_tokens
         self.max_parts = max(1, math.ceil(cfg.max_model_len / self.part_tokens))
+        # small decode batches split the context finer (more workgroups in flight for the
+        # latency-bound B<=2 attention); partial buffers are sized for the finest split
+        self.part_tokens_small = cfg.decode_partition_tokens_small or self.part_tokens
+        self.max_parts_small = max(1, math.ceil(cfg.max_model_len / self.part_tokens_small))
+        if self.max_parts_small > 64:  # in-kernel combine handles <= 64 partitions
+            self.part_tokens_small, self.max_parts_small = self.part_tokens, self.max_parts
+        alloc_parts = max(self.max_parts, self.max_parts_small)
         self.tile_tokens = ops.PREFILL_TILE_TOKENS.get(self.model.g, 16)
         self.graph_sizes = sorted(b for b in cfg.graph_batch_sizes)
         if comm is not None and comm.size > 1 and comm.is_gloo:
@@ -140,9 +147,9 @@ class ModelRunner:
         self.meta_host_np = self.meta_host.numpy()
         self.meta_dev = torch.zeros(self.max_layout.size, dtype=torch.int32, device=self.device)
         nkv = self.model.n_kv_heads
-        self.part_out = torch.empty(self.max_seqs * nkv * self.max_parts * 16 * 128,
+        self.part_out = torch.empty(self.max_seqs * nkv * alloc_parts * 16 * 128,
                                     dtype=torch.float32, device=self.device)
-        self.part_lse = torch.empty(self.max_seqs * nkv * self.max_parts * 16,
+        self.part_lse = torch.empty(self.max_seqs * nkv * alloc_parts * 16,
                                     dtype=torch.float32, device=self.device)
         # fused decode-path workspace (q / attention / activation rows, sampler keys,
         # split-K partials and arrival counters for the decode attention kernel)
@@ -161,7 +168,9 @@ class ModelRunner:
             "max_parts": self.max_parts, "part_tokens": self.part_tokens,
         }
         del H
-        self.fused_decode = bool(cfg.fused_decode)
+        # the fused decode attention combines <= 64 partitions in-kernel (<= 16k tokens at
+        # 256-token partitions); longer contexts use the two-kernel split-K path
+        self.fused_decode = bool(cfg.fused_decode) and self.max_parts <= 64
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_io: dict[int, dict] = {}
         self.graph_pool = None
@@ -209,6 +218,13 @@ class ModelRunner:
         return self.num_blocks * self.block_size
 
     # ------------------------------------------------------------------------------------
+    def _ws_for(self, batch_size: int) -> dict:
+        if batch_size <= self.cfg.decode_small_batch_max and \
+                self.part_tokens_small != self.part_tokens:
+            return {**self.ws, "part_tokens": self.part_tokens_small,
+                    "max_parts": self.max_parts_small}
+        return self.ws
+
     def _prepare(self, batch: Batch, pad_seqs: int = 0, tiles: bool = True):
         ids, qs, ql = batch.arrays()
         d = self.bm.build_batch(ids, qs, ql, self.bt_width,
@@ -249,8 +265,8 @@ class ModelRunner:
         T = v["input_ids"].shape[0]
         if (self.fused_decode and special_sampling is None and md.num_tiles == 0
                 and md.num_decode == T and m.decode_fusable(T)):
-            return m.forward_decode(v["input_ids"], md, self.k_layers, self.v_layers, self.ws,
-                                    v["temperature"], v["seeds"], v["steps"])
+            return m.forward_decode(v["input_ids"], md, self.k_layers, self.v_layers,
+                                    self._ws_for(T), v["temperature"], v["seeds"], v["steps"])
         hidden = m.forward(v["input_ids"], md, self.k_layers, self.v_layers, self.part_out,
                            self.part_lse, num_parts, self.part_tokens)
         last = hidden.index_select(0, v["logits_idx"])

@@ -25,6 +25,8 @@
 //       SAMPLE  logits -> greedy / Gumbel-max key -> one partial max per (row, tile)
 //               (sampler fused into the LM head; `sample_finalize` reduces a row's
 //               partials to its token id with one workgroup per row)
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -312,12 +314,28 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
   }
 }
 
+// Weight-stream cache policy.  Decode reads every weight byte once per step from a 15 GB
+// working set that never fits the 256 MiB Infinity Cache, so non-temporal loads (nt) are the
+// right default; back-to-back microbenchmarks of one matrix (warm MALL) favour the default
+// policy instead and are misleading here.  ATTA_NT_WEIGHTS=0 selects the default policy.
+static bool nt_weights() {
+  static const bool on = [] {
+    const char* e = std::getenv("ATTA_NT_WEIGHTS");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
 template <int WAVES, int UNROLL, int MT, int EPI>
 static void launch_t(int dtype, dim3 grid, hipStream_t st, const SkinnyParams& p) {
-  if (dtype == 0)
-    skinny_kernel<__bf16, WAVES, UNROLL, MT, EPI><<<grid, WAVES * 64, 0, st>>>(p);
-  else
-    skinny_kernel<_Float16, WAVES, UNROLL, MT, EPI><<<grid, WAVES * 64, 0, st>>>(p);
+  const bool nt = nt_weights();
+  if (dtype == 0) {
+    if (nt) skinny_kernel<__bf16, WAVES, UNROLL, MT, EPI, true><<<grid, WAVES * 64, 0, st>>>(p);
+    else skinny_kernel<__bf16, WAVES, UNROLL, MT, EPI, false><<<grid, WAVES * 64, 0, st>>>(p);
+  } else {
+    if (nt) skinny_kernel<_Float16, WAVES, UNROLL, MT, EPI, true><<<grid, WAVES * 64, 0, st>>>(p);
+    else skinny_kernel<_Float16, WAVES, UNROLL, MT, EPI, false><<<grid, WAVES * 64, 0, st>>>(p);
+  }
 }
 
 template <int EPI>
