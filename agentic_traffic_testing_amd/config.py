@@ -159,6 +159,8 @@ class EngineConfig:
     long_prefill_token_threshold: int = 0
     # fused native decode path (GEMV kernels) when available
     fused_decode: bool = True
+    # keep a pre-shuffled copy of the decode-GEMV weights (contiguous 1 KiB wave loads)
+    preshuffle_decode_weights: bool = True
     num_kv_blocks: int = 0               # 0 = size from gpu_memory_utilization
     load_format: str = "auto"            # auto | dummy (random init) | safetensors
     # tensor parallelism: "auto" = RCCL ("nccl") on GPUs, gloo on CPU; "gloo" forces the

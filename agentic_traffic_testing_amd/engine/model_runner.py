@@ -96,7 +96,7 @@ class MetaLayout:
 
 # step-message header (int32 words) shared by rank 0 and the TP workers
 HDR_WORDS = 12
-OP_STEP, OP_CAPTURE, OP_STOP = 1, 2, 3
+OP_STEP, OP_CAPTURE, OP_STOP, OP_BARRIER = 1, 2, 3, 4
 
 
 class ModelRunner:
@@ -117,6 +117,8 @@ class ModelRunner:
             self.model.load_safetensors(weights_dir)
         else:
             self.model.init_random(seed=cfg.seed)
+        if self.is_cuda and cfg.fused_decode and cfg.preshuffle_decode_weights:
+            self.model.prepare_decode_weights()
         self.load_seconds = time.perf_counter() - t0
         self.block_size = cfg.block_size
         self.bt_width = math.ceil(cfg.max_model_len / cfg.block_size)
@@ -346,6 +348,11 @@ class ModelRunner:
             if op == OP_CAPTURE:
                 self.capture(int(hdr[1]))
                 continue
+            if op == OP_BARRIER:
+                if self.is_cuda:
+                    torch.cuda.synchronize(self.device)
+                self.comm.barrier()
+                continue
             size = int(hdr[10])
             self.meta_host_np[:size] = data[HDR_WORDS:HDR_WORDS + size]
             self._run(hdr, worker=True)
@@ -353,6 +360,17 @@ class ModelRunner:
             if self.is_cuda:
                 # meta_host is reused by the next message: drain this step's H2D copy first
                 torch.cuda.current_stream(self.device).synchronize()
+
+    def barrier(self):
+        """Synchronise every TP rank (device work drained, then a process-group barrier)."""
+        if self.is_cuda:
+            torch.cuda.synchronize(self.device)
+        if self.publisher is not None:
+            hdr = np.zeros(HDR_WORDS, dtype=np.int32)
+            hdr[0] = OP_BARRIER
+            self.publisher.publish(hdr)
+        if self.comm is not None:
+            self.comm.barrier()
 
     def stop_workers(self):
         if self.publisher is not None:
@@ -439,4 +457,5 @@ def _discard_sampler(logits):
     return None
 
 
-__all__ = ["ModelRunner", "MetaLayout", "ref", "HDR_WORDS", "OP_STEP", "OP_CAPTURE", "OP_STOP"]
+__all__ = ["ModelRunner", "MetaLayout", "ref", "HDR_WORDS", "OP_STEP", "OP_CAPTURE", "OP_STOP",
+           "OP_BARRIER"]

@@ -61,6 +61,12 @@ class LayerWeights:
     post_norm: torch.Tensor
     gate_up: torch.Tensor
     down: torch.Tensor
+    # decode copies in the GEMV's pre-shuffled layout (ops.preshuffle); None = use the
+    # row-major weights above
+    qkv_ps: torch.Tensor | None = None
+    o_ps: torch.Tensor | None = None
+    gate_up_ps: torch.Tensor | None = None
+    down_ps: torch.Tensor | None = None
 
 
 class LlamaModel:
@@ -84,6 +90,7 @@ class LlamaModel:
         self.vocab_shard = cfg.vocab_size // tp_size
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
         self.layers: list[LayerWeights] = []
+        self.lm_head_ps = None
         self.embed = None
         self.norm = None
         self.lm_head = None
@@ -213,6 +220,22 @@ class LlamaModel:
         self._fold_final_norm()
         return self
 
+    def prepare_decode_weights(self):
+        """Build pre-shuffled copies of every decode-GEMV weight (row-major originals stay
+        for the hipBLASLt prefill GEMMs): each wave load of the decode kernels then reads one
+        contiguous 1 KiB instead of 16 rows x 64 B.  Costs one extra copy of the weights,
+        which 288 GB of HBM affords (16 GB for Llama-3-8B)."""
+        if self.device.type != "cuda":
+            return self
+        for L in self.layers:
+            L.qkv_ps = ops.preshuffle(L.qkv, "qkv")
+            L.o_ps = ops.preshuffle(L.o)
+            L.gate_up_ps = ops.preshuffle(L.gate_up, "silu")
+            L.down_ps = ops.preshuffle(L.down)
+        self.lm_head_ps = ops.preshuffle(self.lm_head)
+        torch.cuda.synchronize(self.device)
+        return self
+
     # ---------------------------------------------------------------------------------
     def weight_bytes(self) -> int:
         n = self.embed.numel() + self.norm.numel() + self.lm_head.numel()
@@ -281,31 +304,41 @@ class LlamaModel:
         attn = ws["attn"][:B]
         act = ws["act"][:B]
         for li, L in enumerate(self.layers):
-            ops.decode_qkv_rope(residual, L.qkv, eps, md.positions, md.slot_mapping, self.cos_sin,
-                                k_caches[li], v_caches[li], nq, nkv, q_out=q)
+            ps = L.qkv_ps is not None
+            ops.decode_qkv_rope(residual, L.qkv_ps if ps else L.qkv, eps, md.positions,
+                                md.slot_mapping, self.cos_sin, k_caches[li], v_caches[li], nq, nkv,
+                                q_out=q, preshuffled=ps)
             ops.attention_decode_v2(q, k_caches[li], v_caches[li], md.block_tables,
                                     md.seq_kvlen, md.seq_qstart, self.scale, ws["part_out"],
                                     ws["part_lse"], ws["counters"], ws["max_parts"],
                                     ws["part_tokens"], out=attn, num_seqs=B)
+            a2 = attn.view(B, nq * self.head_dim)
             if self.tp_size == 1:
-                ops.linear(attn.view(B, nq * self.head_dim), L.o, residual=residual,
-                           waves=ops.WAVES_SMALL)
+                ops.linear(a2, L.o_ps if ps else L.o, residual=residual, waves=ops.WAVES_SMALL,
+                           preshuffled=ps)
             else:
-                residual.add_(self._all_reduce(ops.linear(attn.view(B, nq * self.head_dim), L.o)))
-            ops.decode_gate_up_silu(residual, L.gate_up, eps, out=act)
+                residual.add_(self._all_reduce(ops.linear(a2, L.o_ps if ps else L.o,
+                                                          preshuffled=ps)))
+            ops.decode_gate_up_silu(residual, L.gate_up_ps if ps else L.gate_up, eps, out=act,
+                                    preshuffled=ps)
             if self.tp_size == 1:
-                ops.linear(act, L.down, residual=residual, waves=ops.WAVES_LARGE)
+                ops.linear(act, L.down_ps if ps else L.down, residual=residual,
+                           waves=ops.WAVES_LARGE, preshuffled=ps)
             else:
-                residual.add_(self._all_reduce(ops.linear(act, L.down)))
+                residual.add_(self._all_reduce(ops.linear(act, L.down_ps if ps else L.down,
+                                                          preshuffled=ps)))
+        lm_ps = self.lm_head_ps is not None
+        lm = self.lm_head_ps if lm_ps else self.lm_head
         if self.tp_size == 1:
-            return ops.decode_lm_head_sample(residual, self.lm_head, eps, temperature, seeds,
-                                             steps, ws["keys"], tokens=ws["tokens"][:B])
+            return ops.decode_lm_head_sample(residual, lm, eps, temperature, seeds, steps,
+                                             ws["keys"], tokens=ws["tokens"][:B],
+                                             preshuffled=lm_ps)
         # TP: each rank samples its vocab shard down to one packed key per row (global ids,
         # so the Gumbel noise equals TP=1's); one int64 MAX all-reduce picks the winner
-        keys = ops.decode_lm_head_sample(residual, self.lm_head, eps, temperature, seeds,
-                                         steps, ws["keys"], tokens=ws["tp_keys"][:B],
-                                         finalize="key",
-                                         vocab_offset=self.tp_rank * self.vocab_shard)
+        keys = ops.decode_lm_head_sample(residual, lm, eps, temperature, seeds, steps,
+                                         ws["keys"], tokens=ws["tp_keys"][:B], finalize="key",
+                                         vocab_offset=self.tp_rank * self.vocab_shard,
+                                         preshuffled=lm_ps)
         self.tp_group.all_reduce_max(keys)
         return ops.key_to_token(keys)
 

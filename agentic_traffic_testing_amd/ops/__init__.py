@@ -168,18 +168,60 @@ def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
             and k % 128 == 0 and x.stride(1) == 1 and w.is_contiguous())
 
 
+def preshuffle(w: torch.Tensor, rowmap: str = "plain") -> torch.Tensor:
+    """Re-lay a [N, K] weight for the decode GEMV: rows permuted into the kernel's tile order
+    (``rowmap`` "plain" | "qkv" (RoPE pairs d, d+64 of each 128-dim head in one tile) |
+    "silu" (gate_j and up_j in one tile)), then every 16-row x 32-column block stored as the
+    1 KiB the 64 MFMA lanes load (lane l: row l & 15, columns 8*(l >> 4)..+7).  Same shape
+    and dtype as ``w``; only valid as the ``w`` of ops called with ``preshuffled=True``."""
+    N, K = w.shape
+    if N % 16 or K % 32:
+        raise ValueError(f"preshuffle needs N % 16 == 0 and K % 32 == 0, got {tuple(w.shape)}")
+    dev = w.device
+    if rowmap == "qkv":
+        if N % 128:
+            raise ValueError("qkv rowmap needs whole 128-dim heads")
+        t = torch.arange(N // 16, device=dev)
+        c = torch.arange(16, device=dev)
+        head, j = (t >> 3)[:, None], (t & 7)[:, None]
+        idx = (head * 128 + j * 8 + (c & 7)[None, :] + ((c & 8) != 0)[None, :] * 64).reshape(-1)
+        w = w.index_select(0, idx)
+    elif rowmap == "silu":
+        inter = N // 2
+        if inter % 8:
+            raise ValueError("silu rowmap needs inter % 8 == 0")
+        t = torch.arange(inter // 8, device=dev)[:, None]
+        c = torch.arange(16, device=dev)[None, :]
+        idx = torch.where(c < 8, t * 8 + c, inter + t * 8 + c - 8).reshape(-1)
+        w = w.index_select(0, idx)
+    elif rowmap != "plain":
+        raise ValueError(f"unknown rowmap {rowmap}")
+    return (w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+            .reshape(N, K))
+
+
+def _need_cuda(x, preshuffled):
+    if preshuffled and not x.is_cuda:
+        raise ValueError("pre-shuffled weights are only consumed by the HIP decode kernels")
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None,
-           out: torch.Tensor | None = None, waves: int | None = None) -> torch.Tensor:
+           out: torch.Tensor | None = None, waves: int | None = None,
+           preshuffled: bool = False) -> torch.Tensor:
     """y = x @ w.T.  With ``residual`` the product is added to ``residual`` IN PLACE and
     ``residual`` is returned (residual-stream update).  Decode-sized M runs the MFMA skinny
-    GEMM; everything else (prefill, CPU) runs F.linear (hipBLASLt on the GPU)."""
+    GEMM; everything else (prefill, CPU) runs F.linear (hipBLASLt on the GPU).
+    ``preshuffled``: ``w`` comes from ``preshuffle`` (skinny path only)."""
+    _need_cuda(x, preshuffled)
+    if preshuffled and not skinny_ok(x, w):
+        raise ValueError("pre-shuffled weights need the skinny (decode) path")
     if skinny_ok(x, w):
         if residual is not None:
-            _native().skinny_gemm(residual, x, w, residual, waves or SKINNY_WAVES)
+            _native().skinny_gemm(residual, x, w, residual, waves or SKINNY_WAVES, preshuffled)
             return residual
         if out is None:
             out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
-        _native().skinny_gemm(out, x, w, None, waves or SKINNY_WAVES)
+        _native().skinny_gemm(out, x, w, None, waves or SKINNY_WAVES, preshuffled)
         return out
     y = torch.nn.functional.linear(x, w)
     if residual is not None:
@@ -193,8 +235,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = Non
 
 # ---- fused decode-step ops (norm weight folded into W on the host) -----------------------
 def decode_qkv_rope(x, w, eps, positions, slots, cos_sin, k_cache, v_cache, n_q_heads,
-                    n_kv_heads, q_out=None):
+                    n_kv_heads, q_out=None, preshuffled=False):
     """RMSNorm(x) -> QKV GEMM -> RoPE -> q out + paged K/V write, one kernel on the GPU."""
+    _need_cuda(x, preshuffled)
     if q_out is None:
         q_out = torch.empty(x.shape[0], n_q_heads, 128, dtype=x.dtype, device=x.device)
     if not x.is_cuda:
@@ -204,12 +247,13 @@ def decode_qkv_rope(x, w, eps, positions, slots, cos_sin, k_cache, v_cache, n_q_
         q_out.copy_(q)
         return q_out
     _native().fused_qkv_rope(q_out, k_cache, v_cache, x, w, positions, slots, cos_sin,
-                             n_q_heads, n_kv_heads, eps, WAVES_SMALL)
+                             n_q_heads, n_kv_heads, eps, WAVES_SMALL, preshuffled)
     return q_out
 
 
-def decode_gate_up_silu(x, w, eps, out=None):
+def decode_gate_up_silu(x, w, eps, out=None, preshuffled=False):
     """RMSNorm(x) -> gate_up GEMM -> SiLU(gate) * up, one kernel on the GPU."""
+    _need_cuda(x, preshuffled)
     inter = w.shape[0] // 2
     if out is None:
         out = torch.empty(x.shape[0], inter, dtype=x.dtype, device=x.device)
@@ -217,12 +261,12 @@ def decode_gate_up_silu(x, w, eps, out=None):
         n = ref.rms_norm(x, torch.ones(x.shape[1], dtype=x.dtype), eps)
         out.copy_(ref.silu_and_mul(torch.nn.functional.linear(n, w)))
         return out
-    _native().fused_gate_up_silu(out, x, w, eps, WAVES_LARGE)
+    _native().fused_gate_up_silu(out, x, w, eps, WAVES_LARGE, preshuffled)
     return out
 
 
 def decode_lm_head_sample(x, w, eps, temperature, seeds, steps, keys, tokens=None,
-                          finalize=True, vocab_offset=0):
+                          finalize=True, vocab_offset=0, preshuffled=False):
     """Final RMSNorm -> LM head -> greedy / Gumbel-max sample without materialising logits.
     ``keys`` (int64, >= M * vocab/16 entries) is scratch for the per-tile packed
     (value, index) maxima; no initialisation is needed.
@@ -230,6 +274,7 @@ def decode_lm_head_sample(x, w, eps, temperature, seeds, steps, keys, tokens=Non
     ``finalize``: True -> ``tokens`` gets token ids; ``"key"`` -> ``tokens`` gets each row's
     signed-orderable packed key (TP: MAX all-reduce them, then ``key_to_token``); False ->
     partials only.  ``vocab_offset`` is this shard's first vocab id."""
+    _need_cuda(x, preshuffled)
     if tokens is None:
         tokens = torch.empty(x.shape[0], dtype=torch.long, device=x.device)
     if not x.is_cuda:
@@ -242,7 +287,7 @@ def decode_lm_head_sample(x, w, eps, temperature, seeds, steps, keys, tokens=Non
         return tokens
     mode = 2 if finalize == "key" else (1 if finalize else 0)
     _native().fused_lm_head_sample(tokens, keys, x, w, eps, temperature, seeds, steps, mode,
-                                   vocab_offset, WAVES_LARGE)
+                                   vocab_offset, WAVES_LARGE, preshuffled)
     return tokens
 
 

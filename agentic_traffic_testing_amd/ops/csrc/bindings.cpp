@@ -152,8 +152,13 @@ void sample(at::Tensor out, const at::Tensor& logits, const at::Tensor& temperat
            "sample");
 }
 
+// dtype code for the skinny GEMV entry points; bit 8 flags pre-shuffled weights (kPreshuffled)
+int skinny_dtype(const at::Tensor& x, bool preshuffled) {
+  return dtype_code(x) | (preshuffled ? kPreshuffled : 0);
+}
+
 void skinny_gemm(at::Tensor y, const at::Tensor& x, const at::Tensor& w,
-                 const c10::optional<at::Tensor>& residual, int64_t waves) {
+                 const c10::optional<at::Tensor>& residual, int64_t waves, bool preshuffled) {
   check_dev(x, "x");
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "skinny_gemm: 2-D operands");
   TORCH_CHECK(x.stride(1) == 1 && y.stride(1) == 1 && w.is_contiguous(), "skinny_gemm: layout");
@@ -170,12 +175,13 @@ void skinny_gemm(at::Tensor y, const at::Tensor& x, const at::Tensor& w,
   }
   const at::DeviceGuard g(x.device());
   check_rc(atta_skinny_gemm(y.data_ptr(), x.data_ptr(), w.data_ptr(), r, x.size(0), w.size(0),
-                            w.size(1), x.stride(0), y.stride(0), rs, waves, dtype_code(x),
-                            cur_stream()),
+                            w.size(1), x.stride(0), y.stride(0), rs, waves,
+                            skinny_dtype(x, preshuffled), cur_stream()),
            "skinny_gemm");
 }
 
 void check_skinny(const at::Tensor& x, const at::Tensor& w, const char* what) {
+  TORCH_CHECK(w.size(0) % 16 == 0 && w.size(1) % 32 == 0, what, ": weight tile shape");
   check_dev(x, "x");
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.is_contiguous(), what,
               ": layout");
@@ -185,7 +191,7 @@ void check_skinny(const at::Tensor& x, const at::Tensor& w, const char* what) {
 void fused_qkv_rope(at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache, const at::Tensor& x,
                     const at::Tensor& w, const at::Tensor& positions, const at::Tensor& slots,
                     const at::Tensor& cos_sin, int64_t n_q_heads, int64_t n_kv_heads, double eps,
-                    int64_t waves) {
+                    int64_t waves, bool preshuffled) {
   check_skinny(x, w, "fused_qkv_rope");
   TORCH_CHECK(w.size(0) == (n_q_heads + 2 * n_kv_heads) * 128, "fused_qkv_rope: w rows");
   TORCH_CHECK(positions.scalar_type() == at::kInt && slots.scalar_type() == at::kInt,
@@ -198,27 +204,28 @@ void fused_qkv_rope(at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache, co
                                x.data_ptr(), w.data_ptr(), positions.data_ptr<int>(),
                                slots.data_ptr<int>(), cos_sin.data_ptr<float>(), x.size(0),
                                x.size(1), x.stride(0), q_out.stride(0), n_q_heads, n_kv_heads,
-                               k_cache.size(2), static_cast<float>(eps), waves, dtype_code(x),
-                               cur_stream()),
+                               k_cache.size(2), static_cast<float>(eps), waves,
+                               skinny_dtype(x, preshuffled), cur_stream()),
            "fused_qkv_rope");
 }
 
 void fused_gate_up_silu(at::Tensor out, const at::Tensor& x, const at::Tensor& w, double eps,
-                        int64_t waves) {
+                        int64_t waves, bool preshuffled) {
   check_skinny(x, w, "fused_gate_up_silu");
   TORCH_CHECK(w.size(0) == 2 * out.size(1) && out.size(0) == x.size(0) && out.stride(1) == 1,
               "fused_gate_up_silu: out");
   const at::DeviceGuard g(x.device());
   check_rc(atta_fused_gate_up_silu(out.data_ptr(), x.data_ptr(), w.data_ptr(), x.size(0),
                                    x.size(1), out.size(1), x.stride(0), out.stride(0),
-                                   static_cast<float>(eps), waves, dtype_code(x), cur_stream()),
+                                   static_cast<float>(eps), waves, skinny_dtype(x, preshuffled),
+                                   cur_stream()),
            "fused_gate_up_silu");
 }
 
 void fused_lm_head_sample(at::Tensor tokens, at::Tensor keys, const at::Tensor& x,
                           const at::Tensor& w, double eps, const at::Tensor& temperature,
                           const at::Tensor& seeds, const at::Tensor& steps, int64_t finalize,
-                          int64_t vocab_offset, int64_t waves) {
+                          int64_t vocab_offset, int64_t waves, bool preshuffled) {
   TORCH_CHECK(finalize >= 0 && finalize <= 2, "fused_lm_head_sample: finalize mode 0/1/2");
   check_skinny(x, w, "fused_lm_head_sample");
   TORCH_CHECK(tokens.scalar_type() == at::kLong && keys.scalar_type() == at::kLong &&
@@ -233,8 +240,8 @@ void fused_lm_head_sample(at::Tensor tokens, at::Tensor keys, const at::Tensor& 
                reinterpret_cast<unsigned long long*>(keys.data_ptr<int64_t>()), x.data_ptr(),
                w.data_ptr(), x.size(0), w.size(0), x.size(1), x.stride(0), static_cast<float>(eps),
                temperature.data_ptr<float>(), seeds.data_ptr<int64_t>(), steps.data_ptr<int64_t>(),
-               static_cast<int>(finalize), static_cast<int>(vocab_offset), waves, dtype_code(x),
-               cur_stream()),
+               static_cast<int>(finalize), static_cast<int>(vocab_offset), waves,
+               skinny_dtype(x, preshuffled), cur_stream()),
            "fused_lm_head_sample");
 }
 
@@ -297,14 +304,16 @@ TORCH_LIBRARY(atta, m) {
   m.def(
       "fused_qkv_rope(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor x, "
       "Tensor w, Tensor positions, Tensor slots, Tensor cos_sin, int n_q_heads, int n_kv_heads, "
-      "float eps, int waves) -> ()");
-  m.def("fused_gate_up_silu(Tensor(a!) out, Tensor x, Tensor w, float eps, int waves) -> ()");
+      "float eps, int waves, bool preshuffled=False) -> ()");
+  m.def("fused_gate_up_silu(Tensor(a!) out, Tensor x, Tensor w, float eps, int waves, "
+        "bool preshuffled=False) -> ()");
   m.def(
       "fused_lm_head_sample(Tensor(a!) tokens, Tensor(b!) keys, Tensor x, Tensor w, float eps, "
       "Tensor temperature, Tensor seeds, Tensor steps, int finalize, int vocab_offset, "
-      "int waves) -> ()");
+      "int waves, bool preshuffled=False) -> ()");
   m.def("sample_finalize(Tensor(a!) tokens, Tensor keys, int n_tiles) -> ()");
-  m.def("skinny_gemm(Tensor(a!) y, Tensor x, Tensor w, Tensor? residual, int waves) -> ()");
+  m.def("skinny_gemm(Tensor(a!) y, Tensor x, Tensor w, Tensor? residual, int waves, "
+        "bool preshuffled=False) -> ()");
   m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rms_norm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");

@@ -89,6 +89,7 @@ struct SkinnyParams {
   unsigned long long* keys;  // [M, key_stride] per-tile partial maxima
   int key_stride;
   int vocab_offset;          // first vocab id of this TP rank's LM-head shard
+  int ps;                    // weights pre-shuffled into the MFMA lane order (see preshuffle)
   const float* temperature;
   const int64_t* seeds;
   const int64_t* steps;
@@ -118,7 +119,13 @@ __device__ __forceinline__ int tile_row(int tile, int c, const SkinnyParams& p) 
   }
 }
 
-template <typename T, int WAVES, int UNROLL, int MT, int EPI, bool NTL = false>
+// Weight layouts.  Row-major [N][K]: a wave's 16-byte-per-lane load touches 16 rows x 64 B
+// (16 DRAM pages per instruction).  Pre-shuffled (PS): for every 16-row tile (rows already
+// permuted by tile_row<EPI>) and every 32-wide K step, the 16 x 32 block is stored as the
+// 1 KiB the 64 lanes read - lane l at byte 16*l holds row (l & 15), k 8*(l >> 4)..+7 - so
+// each wave load instruction is one contiguous 1 KiB and a wave streams a contiguous
+// range.  ops.preshuffle builds it once at weight-load time.
+template <typename T, int WAVES, int UNROLL, int MT, int EPI, bool NTL = false, bool PS = false>
 __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
   using MF = MfmaK32<T>;
   using frag8 = typename MF::frag8;
@@ -135,7 +142,11 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
   const int kw = p.K / WAVES;
   const int kbeg = wid * kw;
   const int wrow = tile_row<EPI>(tile, col, p);
-  const uint16_t* wp = p.w + static_cast<int64_t>(wrow) * p.K + kbeg + 8 * grp;
+  const uint16_t* wp =
+      PS ? p.w + (static_cast<int64_t>(tile) * (p.K / 32) + kbeg / 32) * 512 + lane * 8
+         : p.w + static_cast<int64_t>(wrow) * p.K + kbeg + 8 * grp;
+  // element offset of K-offset k (a multiple of 32) from wp in either layout
+  auto woff = [](int k) { return PS ? k * 16 : k; };
   const uint16_t* xp[MT];
   bool xv[MT];
 #pragma unroll
@@ -159,9 +170,9 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u)
       if constexpr (NTL)
-        f[u] = __builtin_nontemporal_load(reinterpret_cast<const frag8*>(wp + k + 32 * u));
+        f[u] = __builtin_nontemporal_load(reinterpret_cast<const frag8*>(wp + woff(k + 32 * u)));
       else
-        f[u] = *reinterpret_cast<const frag8*>(wp + k + 32 * u);
+        f[u] = *reinterpret_cast<const frag8*>(wp + woff(k + 32 * u));
   };
   auto compute = [&](const frag8 (&f)[UNROLL], int k) {
 #pragma unroll
@@ -190,7 +201,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
     if (s < nsteps) compute(wa, s * STEP);
   }
   for (int k = nsteps * STEP; k < kw; k += 32) {  // tail (K not a multiple of the stage)
-    const frag8 wf = *reinterpret_cast<const frag8*>(wp + k);
+    const frag8 wf = *reinterpret_cast<const frag8*>(wp + woff(k));
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       const frag8 xf = xv[t] ? *reinterpret_cast<const frag8*>(xp[t] + k) : frag8{};
@@ -314,14 +325,13 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
   }
 }
 
-// Weight-stream cache policy.  Decode reads every weight byte once per step from a 15 GB
-// working set that never fits the 256 MiB Infinity Cache, so non-temporal loads (nt) are the
-// right default; back-to-back microbenchmarks of one matrix (warm MALL) favour the default
-// policy instead and are misleading here.  ATTA_NT_WEIGHTS=0 selects the default policy.
+// Weight-stream cache policy.  Measured on the fan-out bench (profiles/bench_r1_ab_nt.log):
+// register-destination nt loads made every decode GEMV slower (gate_up 42 -> 48 us, down
+// 23 -> 29 us), so the default policy stays; ATTA_NT_WEIGHTS=1 re-enables nt for A/B runs.
 static bool nt_weights() {
   static const bool on = [] {
     const char* e = std::getenv("ATTA_NT_WEIGHTS");
-    return e == nullptr || e[0] != '0';
+    return e != nullptr && e[0] == '1';
   }();
   return on;
 }
@@ -329,12 +339,15 @@ static bool nt_weights() {
 template <int WAVES, int UNROLL, int MT, int EPI>
 static void launch_t(int dtype, dim3 grid, hipStream_t st, const SkinnyParams& p) {
   const bool nt = nt_weights();
+  const dim3 blk(WAVES * 64);
   if (dtype == 0) {
-    if (nt) skinny_kernel<__bf16, WAVES, UNROLL, MT, EPI, true><<<grid, WAVES * 64, 0, st>>>(p);
-    else skinny_kernel<__bf16, WAVES, UNROLL, MT, EPI, false><<<grid, WAVES * 64, 0, st>>>(p);
+    if (p.ps) skinny_kernel<__bf16, WAVES, UNROLL, MT, EPI, false, true><<<grid, blk, 0, st>>>(p);
+    else if (nt) skinny_kernel<__bf16, WAVES, UNROLL, MT, EPI, true><<<grid, blk, 0, st>>>(p);
+    else skinny_kernel<__bf16, WAVES, UNROLL, MT, EPI, false><<<grid, blk, 0, st>>>(p);
   } else {
-    if (nt) skinny_kernel<_Float16, WAVES, UNROLL, MT, EPI, true><<<grid, WAVES * 64, 0, st>>>(p);
-    else skinny_kernel<_Float16, WAVES, UNROLL, MT, EPI, false><<<grid, WAVES * 64, 0, st>>>(p);
+    if (p.ps) skinny_kernel<_Float16, WAVES, UNROLL, MT, EPI, false, true><<<grid, blk, 0, st>>>(p);
+    else if (nt) skinny_kernel<_Float16, WAVES, UNROLL, MT, EPI, true><<<grid, blk, 0, st>>>(p);
+    else skinny_kernel<_Float16, WAVES, UNROLL, MT, EPI, false><<<grid, blk, 0, st>>>(p);
   }
 }
 
@@ -420,9 +433,12 @@ static int skinny_checks(int M, int K, int waves) {
 int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual, int M, int N,
                      int K, int64_t x_stride, int64_t y_stride, int64_t res_stride, int waves,
                      int dtype, hipStream_t stream) {
+  const int ps = (dtype & kPreshuffled) ? 1 : 0;
+  dtype &= ~kPreshuffled;
   waves = fit_waves(waves, K);
   if (skinny_checks(M, K, waves) || N % 16 != 0) return -1;
   SkinnyParams p{};
+  p.ps = ps;
   p.x = static_cast<const uint16_t*>(x);
   p.w = static_cast<const uint16_t*>(w);
   p.M = M;
@@ -451,12 +467,15 @@ int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x
                         const int* positions, const int* slots, const float* cos_sin, int M,
                         int K, int64_t x_stride, int64_t q_stride, int n_q_heads, int n_kv_heads,
                         int block_size, float eps, int waves, int dtype, hipStream_t stream) {
+  const int ps = (dtype & kPreshuffled) ? 1 : 0;
+  dtype &= ~kPreshuffled;
   waves = fit_waves(waves, K);
   if (skinny_checks(M, K, waves)) return -1;
   int shift = 0;
   while ((1 << shift) < block_size) ++shift;
   if ((1 << shift) != block_size) return -1;
   SkinnyParams p{};
+  p.ps = ps;
   p.x = static_cast<const uint16_t*>(x);
   p.w = static_cast<const uint16_t*>(w);
   p.y = static_cast<uint16_t*>(q_out);
@@ -482,9 +501,12 @@ int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x
 int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int K, int inter,
                             int64_t x_stride, int64_t out_stride, float eps, int waves, int dtype,
                             hipStream_t stream) {
+  const int ps = (dtype & kPreshuffled) ? 1 : 0;
+  dtype &= ~kPreshuffled;
   waves = fit_waves(waves, K);
   if (skinny_checks(M, K, waves) || inter % 8 != 0) return -1;
   SkinnyParams p{};
+  p.ps = ps;
   p.x = static_cast<const uint16_t*>(x);
   p.w = static_cast<const uint16_t*>(w);
   p.y = static_cast<uint16_t*>(out);
@@ -505,9 +527,12 @@ int atta_fused_lm_head_sample(int64_t* tokens, unsigned long long* keys, const v
                               const float* temperature, const int64_t* seeds,
                               const int64_t* steps, int finalize, int vocab_offset,
                               int waves, int dtype, hipStream_t stream) {
+  const int ps = (dtype & kPreshuffled) ? 1 : 0;
+  dtype &= ~kPreshuffled;
   waves = fit_waves(waves, K);
   if (skinny_checks(M, K, waves) || N % 16 != 0) return -1;
   SkinnyParams p{};
+  p.ps = ps;
   p.x = static_cast<const uint16_t*>(x);
   p.w = static_cast<const uint16_t*>(w);
   p.x_stride = x_stride;
@@ -544,8 +569,8 @@ int atta_skinny_variant(void* y, const void* x, const void* w, int M, int N, int
   p.K = K;
   if (M < 1 || M > 16 || N % 16) return -1;
   dim3 grid(N / 16);
-  static const int waves_of[8] = {8, 8, 4, 4, 8, 16, 8, 16};
-  if (K % (32 * waves_of[variant & 7])) return -1;
+  static const int waves_of[10] = {8, 8, 4, 4, 8, 16, 8, 16, 8, 16};
+  if (variant < 0 || variant > 9 || K % (32 * waves_of[variant])) return -1;
   switch (variant) {
     case 0: skinny_kernel<__bf16, 8, 4, 1, EPI_PLAIN, true><<<grid, 512, 0, stream>>>(p); break;
     case 1: skinny_kernel<__bf16, 8, 8, 1, EPI_PLAIN, false><<<grid, 512, 0, stream>>>(p); break;
@@ -555,6 +580,9 @@ int atta_skinny_variant(void* y, const void* x, const void* w, int M, int N, int
     case 5: skinny_kernel<__bf16, 16, 4, 1, EPI_PLAIN, false><<<grid, 1024, 0, stream>>>(p); break;
     case 6: skinny_kernel<__bf16, 8, 2, 1, EPI_PLAIN, false><<<grid, 512, 0, stream>>>(p); break;
     case 7: skinny_kernel<__bf16, 16, 2, 1, EPI_PLAIN, false><<<grid, 1024, 0, stream>>>(p); break;
+    // 8 / 9: pre-shuffled weights (w must come from ops.preshuffle)
+    case 8: skinny_kernel<__bf16, 8, 2, 1, EPI_PLAIN, false, true><<<grid, 512, 0, stream>>>(p); break;
+    case 9: skinny_kernel<__bf16, 16, 2, 1, EPI_PLAIN, false, true><<<grid, 1024, 0, stream>>>(p); break;
     default: return -1;
   }
   return static_cast<int>(hipGetLastError());

@@ -3,6 +3,10 @@
 // synchronisation) and returns 0 on success, -1 for an unsupported shape, or a hipError_t.
 // dtype: 0 = bf16, 1 = fp16.
 #pragma once
+
+// OR-ed into the dtype code of the skinny GEMV entry points: weights are pre-shuffled
+// into the MFMA lane order (ops.preshuffle).
+constexpr int kPreshuffled = 256;
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

@@ -304,10 +304,9 @@ def create_app(state: ServerState) -> web.Application:
     return app
 
 
-def build_engine(args):
-    """Build the (possibly tensor-parallel) engine from CLI args + env fallbacks."""
+def build_config(args):
+    """EngineConfig from CLI args + env fallbacks (reference env knobs, compose defaults)."""
     from ..config import EngineConfig
-    from ..engine.llm_engine import LLMEngine
 
     kw = dict(model=args.model)
     if args.max_model_len:
@@ -329,11 +328,20 @@ def build_engine(args):
     kw["load_format"] = args.load_format
     if args.device:
         kw["device"] = args.device
-    cfg = EngineConfig.from_env(**kw)
+    return EngineConfig.from_env(**kw)
+
+
+def build_engine(args):
+    """Build the (possibly tensor-parallel) engine from CLI args + env fallbacks."""
+    from ..engine.llm_engine import LLMEngine
+
+    cfg = build_config(args)
     if cfg.tensor_parallel_size > 1:
         from ..parallel.tp_engine import TPEngine
 
-        return TPEngine(cfg)
+        # under torchrun (WORLD_SIZE set) the other ranks were started by the launcher
+        external = int(os.environ.get("WORLD_SIZE", "1")) == cfg.tensor_parallel_size
+        return TPEngine(cfg, external=external)
     eng = LLMEngine(cfg)
     eng.runner.capture_all()
     return eng
@@ -387,6 +395,9 @@ def make_parser() -> argparse.ArgumentParser:
     p.add_argument("--max-num-batched-tokens", type=int, default=None)
     p.add_argument("--gpu-memory-utilization", type=float, default=None)
     p.add_argument("--tensor-parallel-size", "--tp-size", type=int, default=None)
+    p.add_argument("--data-parallel-size", "--dp-size", type=int, default=1,
+                   help="engine replicas, one per GPU, behind a router on --port "
+                        "(parallel/dp_router.py)")
     p.add_argument("--block-size", type=int, default=None)
     p.add_argument("--no-prefix-caching", action="store_true")
     p.add_argument("--no-graphs", action="store_true")
@@ -418,8 +429,40 @@ def apply_config_file(args):
     return args
 
 
+def _tp_worker_rank(args) -> bool:
+    """torchrun launch of a TP group: ranks > 0 replay rank 0's steps and never serve."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world <= 1 or rank == 0:
+        return False
+    from ..parallel.tp_engine import run_worker
+
+    cfg = build_config(args)
+    run_worker(cfg, rank, world, int(os.environ.get("MASTER_PORT", "29511")))
+    return True
+
+
 def main(argv=None) -> None:
     args = apply_config_file(make_parser().parse_args(argv))
+    if args.data_parallel_size and args.data_parallel_size > 1:
+        from ..parallel import dp_router
+
+        raw = list(sys.argv[1:] if argv is None else argv)
+        fwd, skip = [], False
+        for i, a in enumerate(raw):  # drop router-level flags, forward the engine flags
+            if skip:
+                skip = False
+                continue
+            if a in ("--data-parallel-size", "--dp-size", "--port", "--host"):
+                skip = True
+                continue
+            if a.startswith(("--data-parallel-size=", "--dp-size=", "--port=", "--host=")):
+                continue
+            fwd.append(a)
+        sys.exit(dp_router.main(["--host", args.host, "--port", str(args.port),
+                                 "--num-replicas", str(args.data_parallel_size), *fwd]))
+    if _tp_worker_rank(args):
+        return
     try:
         asyncio.run(run_server(args))
     except KeyboardInterrupt:

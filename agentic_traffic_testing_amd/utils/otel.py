@@ -2,9 +2,10 @@
 
 The reference uses the OpenTelemetry SDK with an OTLP/HTTP exporter to Jaeger
 (agents/common/tracing.py:16-37, llm/tracing.py:14-28) and embeds span ids in JSON
-responses (``span_to_metadata``, agents/common/tracing.py:50-85).  When the
-``opentelemetry`` packages are importable this module delegates to them; otherwise it
-provides a small self-contained implementation with the same surface:
+responses (``span_to_metadata``, agents/common/tracing.py:50-85).  The SDK is not part of
+this image, so this module is a small self-contained implementation of the surface the
+testbed uses, speaking the same wire formats (W3C trace-context headers, OTLP/HTTP JSON), so
+Jaeger and any OpenTelemetry-instrumented peer interoperate with it:
 
 * ``get_tracer(name)`` -> tracer with ``start_as_current_span(name, context=, kind=)`` and
   ``start_span``; spans carry ``set_attribute``, ``get_span_context()``, ``attributes``;

@@ -9,6 +9,10 @@ generating exactly ``--max-tokens`` (512) tokens with temperature 0.2.  With N G
 (data-parallel serving, weak scaling) on its own GPU; the reported value is the whole-job
 completion tokens/s (sum over ranks / slowest rank's wall time).
 
+``--parallel tp`` instead runs ONE engine tensor-parallel over the N ranks (rank 0 drives the
+workload; the other ranks replay its steps, parallel/tp_engine.py) - the TP scaling curve
+BASELINE.md asks for next to the replica (dp) curve; that mode is strong scaling.
+
 Weights are seeded random-init of the exact Llama-3.1-8B architecture and prompts are
 synthetic (no network / gated checkpoints), which ``data`` states.
 
@@ -45,7 +49,11 @@ def main():
     ap.add_argument("--dtype", default="bfloat16")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--parallel", choices=["dp", "tp"], default="dp",
+                    help="dp: one engine replica per GPU (default); tp: one engine over all GPUs")
     a = ap.parse_args()
+    if a.parallel == "tp" and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        return main_tp(a)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -158,6 +166,57 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def main_tp(a):
+    """Tensor-parallel bench: ranks > 0 serve rank 0's steps until it stops them."""
+    world = int(os.environ["WORLD_SIZE"])
+    rank = int(os.environ.get("RANK", "0"))
+    from agentic_traffic_testing_amd.config import EngineConfig
+
+    cfg = EngineConfig(model=a.model, dtype=a.dtype, max_model_len=a.max_model_len,
+                       max_num_seqs=a.max_num_seqs,
+                       max_num_batched_tokens=a.max_num_batched_tokens,
+                       gpu_memory_utilization=a.gpu_memory_utilization,
+                       use_graphs=not a.no_graphs, seed=1234, device="cuda",
+                       tensor_parallel_size=world)
+    port = int(os.environ.get("MASTER_PORT", "29511"))
+    if rank > 0:
+        from agentic_traffic_testing_amd.parallel.tp_engine import run_worker
+
+        run_worker(cfg, rank, world, port)
+        return
+    from agentic_traffic_testing_amd.bench.fanout import FanoutWorkload
+    from agentic_traffic_testing_amd.parallel.tp_engine import TPEngine
+
+    t0 = time.perf_counter()
+    eng = TPEngine(cfg, external=True)
+    init_s = time.perf_counter() - t0
+    wl = FanoutWorkload(eng, fanout=a.fanout, max_tokens=a.max_tokens, seed=0)
+    for _ in range(a.warmup):
+        wl.run_episode()
+    eng.runner.barrier()
+    t_start = time.perf_counter()
+    results = [wl.run_episode() for _ in range(a.steps)]
+    eng.runner.barrier()
+    elapsed = time.perf_counter() - t_start
+    tokens = sum(r.completion_tokens for r in results)
+    ttfts = sorted(t for r in results for t in r.ttfts)
+    out = {
+        "metric": METRIC, "value": round(tokens / elapsed, 2), "unit": "tokens/s",
+        "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1000.0, 2), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "bf16" if "bf" in a.dtype else a.dtype,
+        "data": "synthetic (agent fan-out prompts, synthetic tokenizer, seeded random-init "
+                "Llama-3.1-8B weights)",
+        "config": {"model": "Llama-3.1-8B (random-init)", "global_batch": a.fanout,
+                   "seq_len": a.max_model_len, "parallelism": f"tp{world}",
+                   "max_tokens": a.max_tokens, "hipgraphs": not a.no_graphs},
+        "p50_ttft_s": round(statistics.median(ttfts), 4) if ttfts else None,
+        "completion_tokens": int(tokens), "init_s": round(init_s, 1),
+    }
+    print(json.dumps(out), flush=True)
+    eng.shutdown()
 
 
 if __name__ == "__main__":

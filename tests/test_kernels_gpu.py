@@ -344,3 +344,52 @@ def test_attention_decode_v2(hq, hkv, part_tokens):
                                 part_tokens, out=out)
         close(out[:-1], exp[:-1], 1.5e-2, 2e-2)
         assert bool((cnt == 0).all())
+
+
+@pytest.mark.parametrize("m", [1, 5, 20])
+def test_preshuffled_decode_kernels_bit_identical(m):
+    """Pre-shuffled weights feed the same lanes the same products in the same order, so every
+    fused decode kernel must return bit-identical results to the row-major layout."""
+    torch.manual_seed(21)
+    dt, H, bs = torch.bfloat16, 1024, 16
+    x = torch.randn(m, H, dtype=dt, device="cuda")
+    # plain GEMM + residual
+    w = torch.randn(2048, H, dtype=dt, device="cuda") * 0.05
+    wp = ops.preshuffle(w)
+    assert torch.equal(ops.linear(x, w), ops.linear(x, wp, preshuffled=True))
+    r1 = torch.randn(m, 2048, dtype=dt, device="cuda")
+    r2 = r1.clone()
+    ops.linear(x, w, residual=r1)
+    ops.linear(x, wp, residual=r2, preshuffled=True)
+    assert torch.equal(r1, r2)
+    # gate_up + SiLU
+    inter = 512
+    wg = torch.randn(2 * inter, H, dtype=dt, device="cuda") * 0.05
+    a = ops.decode_gate_up_silu(x, wg, 1e-5)
+    b = ops.decode_gate_up_silu(x, ops.preshuffle(wg, "silu"), 1e-5, preshuffled=True)
+    assert torch.equal(a, b)
+    # qkv + RoPE + paged KV write
+    hq, hkv = 8, 2
+    wq = torch.randn((hq + 2 * hkv) * 128, H, dtype=dt, device="cuda") * 0.05
+    nb = 8
+    kc1 = torch.zeros(nb, hkv, bs, 128, dtype=dt, device="cuda")
+    vc1 = torch.zeros(nb, hkv, 128, bs, dtype=dt, device="cuda")
+    kc2, vc2 = kc1.clone(), vc1.clone()
+    pos = torch.arange(m, dtype=torch.int32, device="cuda") + 3
+    slots = torch.arange(m, dtype=torch.int32, device="cuda") * 5
+    cs = ref.rope_cos_sin(128, 64, 500000.0, None, device="cuda")
+    q1 = ops.decode_qkv_rope(x, wq, 1e-5, pos, slots, cs, kc1, vc1, hq, hkv)
+    q2 = ops.decode_qkv_rope(x, ops.preshuffle(wq, "qkv"), 1e-5, pos, slots, cs, kc2, vc2, hq,
+                             hkv, preshuffled=True)
+    assert torch.equal(q1, q2) and torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
+    # LM head + sampler
+    V = 4096
+    wl = torch.randn(V, H, dtype=dt, device="cuda") * 0.05
+    keys = torch.empty(m * V // 16, dtype=torch.int64, device="cuda")
+    temp = torch.full((m,), 0.5, device="cuda")
+    seeds = torch.arange(m, dtype=torch.int64, device="cuda")
+    steps = torch.zeros(m, dtype=torch.int64, device="cuda")
+    t1 = ops.decode_lm_head_sample(x, wl, 1e-5, temp, seeds, steps, keys).clone()
+    t2 = ops.decode_lm_head_sample(x, ops.preshuffle(wl), 1e-5, temp, seeds, steps, keys,
+                                   preshuffled=True)
+    assert torch.equal(t1, t2)
