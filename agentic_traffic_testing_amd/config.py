@@ -151,9 +151,10 @@ class EngineConfig:
     graph_batch_sizes: tuple = (1, 2, 4, 8, 16, 32, 64, 128, 256)
     # decode split-K partition size (tokens) for the paged attention kernel
     decode_partition_tokens: int = 256
-    # finer split for small decode batches (<= decode_small_batch_max sequences): B=1 steps
-    # are latency-bound and gain from more workgroups (profiles/r1_microbench_v4_tuned.txt)
-    decode_partition_tokens_small: int = 128
+    # optional finer split for small decode batches (<= decode_small_batch_max sequences).
+    # Off (0): 128-token partitions won in the isolated microbenchmark but lost inside the
+    # real decode step (13.8 vs 12.3 us, profiles/r1_profile_v6_preshuffled.txt)
+    decode_partition_tokens_small: int = 0
     decode_small_batch_max: int = 2
     # chunked prefill: max prompt tokens of one sequence per step (0 = max_num_batched_tokens)
     long_prefill_token_threshold: int = 0

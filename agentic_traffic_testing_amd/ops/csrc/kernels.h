@@ -72,3 +72,14 @@ int atta_attention_decode_v2(void* out, float* part_out, float* part_lse, int* c
 
 int atta_skinny_variant(void* y, const void* x, const void* w, int M, int N, int K,
                         int variant, hipStream_t stream);
+
+// ---- one-shot IPC all-reduce (allreduce.hip) ---------------------------------------------
+size_t atta_ar_buffer_bytes(int64_t max_elems, int elem_bytes);
+int atta_ar_alloc(void** ptr, size_t bytes);
+int atta_ar_free(void* ptr);
+int atta_ar_handle_bytes();
+int atta_ar_ipc_handle(void* ptr, void* handle_out);
+int atta_ar_ipc_open(const void* handle, void** ptr);
+int atta_ar_ipc_close(void* ptr);
+int atta_ar_run(void* const* bases, int rank, int world, int64_t max_elems, const void* x,
+                void* y, int64_t n, int dtype, hipStream_t stream);
