@@ -9,7 +9,7 @@
 // Buffer of one rank (hipExtMallocWithFlags(hipDeviceMallocUncached): peer stores land in
 // memory and local loads bypass the non-coherent caches):
 //   [flags   : 2 parities x kMaxRanks x kMaxBlocks uint32] written by peers
-//   [counters: kMaxBlocks uint32]                            this rank's per-block generation
+//   [counters: kMaxBlocks uint32 + 1 error word]             this rank's per-block generation
 //   [data    : 2 parities x kMaxRanks x max_elems T]        slot (parity, src rank)
 // Every launch uses the same fixed grid, so the per-block generation counters advance in
 // lockstep and form one global generation g per call; call g uses parity g & 1 for ALL of its
@@ -88,9 +88,17 @@ __global__ void __launch_bounds__(kThreads) oneshot_kernel(Params p, const uint1
     __hip_atomic_store(flag_ptr(p.base[threadIdx.x], par, p.rank, b), gen, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t* f = flag_ptr(mine, par, threadIdx.x, b);
+    // bounded wait (~2-4 s): a dead peer must not hang the GPU; the block then records the
+    // failure in the error word and finishes (the result is garbage, the host checks it)
+    uint32_t spins = 0;
     while (static_cast<int32_t>(__hip_atomic_load(f, __ATOMIC_ACQUIRE,
-                                                  __HIP_MEMORY_SCOPE_SYSTEM) - gen) < 0)
-      __builtin_amdgcn_s_sleep(1);
+                                                  __HIP_MEMORY_SCOPE_SYSTEM) - gen) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 25)) {
+        atomicOr(counters + kMaxBlocks, 1u << threadIdx.x);
+        break;
+      }
+    }
   }
   __syncthreads();
   // 4) reduce the W slots in rank order (fp32) into y
@@ -164,6 +172,11 @@ int atta_ar_ipc_open(const void* handle, void** ptr) {
 int atta_ar_ipc_close(void* ptr) { return static_cast<int>(hipIpcCloseMemHandle(ptr)); }
 
 int atta_ar_handle_bytes() { return static_cast<int>(sizeof(hipIpcMemHandle_t)); }
+
+// Byte offset of the error word (bit q set: timed out waiting for rank q).
+int64_t atta_ar_error_offset() {
+  return static_cast<int64_t>(ar::kFlagBytes + ar::kMaxBlocks * sizeof(uint32_t));
+}
 
 int atta_ar_run(void* const* bases, int rank, int world, int64_t max_elems, const void* x, void* y,
                 int64_t n, int dtype, hipStream_t stream) {

@@ -292,9 +292,73 @@ void skinny_variant(at::Tensor y, const at::Tensor& x, const at::Tensor& w, int6
            "skinny_variant");
 }
 
+// ---- one-shot IPC all-reduce -------------------------------------------------------------
+// Buffers are raw device allocations (uncached, IPC-exportable) addressed by int64 pointers;
+// the Python side (parallel/custom_allreduce.py) owns their lifetime.
+int64_t ar_buffer_bytes(int64_t max_elems, int64_t elem_bytes) {
+  return static_cast<int64_t>(atta_ar_buffer_bytes(max_elems, static_cast<int>(elem_bytes)));
+}
+
+int64_t ar_alloc(int64_t bytes, int64_t device) {
+  hipSetDevice(static_cast<int>(device));
+  void* p = nullptr;
+  check_rc(atta_ar_alloc(&p, static_cast<size_t>(bytes)), "ar_alloc");
+  return reinterpret_cast<int64_t>(p);
+}
+
+void ar_free(int64_t ptr) { check_rc(atta_ar_free(reinterpret_cast<void*>(ptr)), "ar_free"); }
+
+at::Tensor ar_handle(int64_t ptr) {
+  at::Tensor h = at::zeros({atta_ar_handle_bytes()}, at::TensorOptions().dtype(at::kByte));
+  check_rc(atta_ar_ipc_handle(reinterpret_cast<void*>(ptr), h.data_ptr()), "ar_handle");
+  return h;
+}
+
+int64_t ar_open(const at::Tensor& handle) {
+  TORCH_CHECK(!handle.is_cuda() && handle.scalar_type() == at::kByte &&
+                  handle.numel() == atta_ar_handle_bytes(), "ar_open: CPU uint8 IPC handle");
+  void* p = nullptr;
+  check_rc(atta_ar_ipc_open(handle.contiguous().data_ptr(), &p), "ar_open");
+  return reinterpret_cast<int64_t>(p);
+}
+
+int64_t ar_error(int64_t ptr) {
+  uint32_t word = 0;
+  check_rc(static_cast<int>(hipMemcpy(&word, reinterpret_cast<uint8_t*>(ptr) + atta_ar_error_offset(),
+                                      sizeof(word), hipMemcpyDeviceToHost)),
+           "ar_error");
+  return word;
+}
+
+void ar_close(int64_t ptr) {
+  check_rc(atta_ar_ipc_close(reinterpret_cast<void*>(ptr)), "ar_close");
+}
+
+void ar_run(const at::Tensor& x, at::Tensor y, at::IntArrayRef bases, int64_t rank,
+            int64_t max_elems) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel() &&
+                  x.scalar_type() == y.scalar_type(), "ar_run: layout");
+  TORCH_CHECK(bases.size() >= 2 && bases.size() <= 8, "ar_run: 2..8 ranks");
+  void* b[8] = {};
+  for (size_t i = 0; i < bases.size(); ++i) b[i] = reinterpret_cast<void*>(bases[i]);
+  const at::DeviceGuard g(x.device());
+  check_rc(atta_ar_run(b, static_cast<int>(rank), static_cast<int>(bases.size()), max_elems,
+                       x.data_ptr(), y.data_ptr(), x.numel(), dtype_code(x), cur_stream()),
+           "ar_run");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(atta, m) {
+  m.def("ar_buffer_bytes(int max_elems, int elem_bytes) -> int", &ar_buffer_bytes);
+  m.def("ar_alloc(int bytes, int device) -> int", &ar_alloc);
+  m.def("ar_free(int ptr) -> ()", &ar_free);
+  m.def("ar_handle(int ptr) -> Tensor", &ar_handle);
+  m.def("ar_open(Tensor handle) -> int", &ar_open);
+  m.def("ar_close(int ptr) -> ()", &ar_close);
+  m.def("ar_error(int ptr) -> int", &ar_error);
+  m.def("ar_run(Tensor x, Tensor(a!) y, int[] bases, int rank, int max_elems) -> ()");
   m.def("skinny_variant(Tensor(a!) y, Tensor x, Tensor w, int variant) -> ()");
   m.def(
       "attention_decode_v2(Tensor(a!) out, Tensor(b!) part_out, Tensor(c!) part_lse, "
@@ -334,6 +398,7 @@ TORCH_LIBRARY(atta, m) {
 }
 
 TORCH_LIBRARY_IMPL(atta, CUDA, m) {
+  m.impl("ar_run", &ar_run);
   m.impl("rms_norm", &rms_norm);
   m.impl("fused_add_rms_norm", &fused_add_rms_norm);
   m.impl("silu_and_mul", &silu_and_mul);

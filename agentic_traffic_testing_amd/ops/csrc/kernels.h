@@ -78,6 +78,7 @@ size_t atta_ar_buffer_bytes(int64_t max_elems, int elem_bytes);
 int atta_ar_alloc(void** ptr, size_t bytes);
 int atta_ar_free(void* ptr);
 int atta_ar_handle_bytes();
+int64_t atta_ar_error_offset();
 int atta_ar_ipc_handle(void* ptr, void* handle_out);
 int atta_ar_ipc_open(const void* handle, void** ptr);
 int atta_ar_ipc_close(void* ptr);

@@ -131,3 +131,68 @@ def test_tp2_same_gpu_rehearsal():
     # bf16 partial sums split across ranks round differently: allow a late near-tie flip
     assert all(g[:2] == e[:2] for g, e in zip(got, exp)), (got, exp)
     assert sum(g == e for g, e in zip(got, exp)) >= 2, (got, exp)
+
+
+def _ipc_ar_worker(rank, world, port, q):
+    try:
+        from agentic_traffic_testing_amd.parallel.comm import init_distributed
+        from agentic_traffic_testing_amd.parallel.custom_allreduce import IpcAllReduce
+
+        torch.cuda.set_device(0)
+        comm = init_distributed(rank, world, "cuda:0", "gloo", "127.0.0.1", port)
+        ar = IpcAllReduce(comm, "cuda:0", max_bytes=16 * 8192 * 2)
+        bad = []
+        for it, n in enumerate([8, 7, 4096, 8192 * 5 + 3, 16 * 8192, 1000, 4096] * 6):
+            g = torch.Generator(device="cpu").manual_seed(1000 * it)
+            parts = [torch.randn(n, generator=g).to(torch.bfloat16) for _ in range(world)]
+            exp = torch.zeros(n)
+            for p_ in parts:  # rank order, fp32, like the kernel
+                exp += p_.float()
+            x = parts[rank].cuda()
+            ar.all_reduce(x)
+            torch.cuda.synchronize()
+            if not torch.equal(x.cpu(), exp.to(torch.bfloat16)):
+                bad.append((it, n))
+        # graph-captured replays with fresh inputs each time
+        x = torch.empty(4096, dtype=torch.bfloat16, device="cuda")
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            ar.all_reduce(x.fill_(1.0))
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            ar.all_reduce(x)
+        for k in range(5):
+            x.fill_(float(rank + k))
+            graph.replay()
+            torch.cuda.synchronize()
+            want = float(sum(r + k for r in range(world)))
+            if not bool((x == want).all()):
+                bad.append(("graph", k, float(x[0])))
+        if ar.check() != 0:
+            bad.append(("timeout-word", ar.check()))
+        comm.barrier()
+        ar.close()
+        q.put((rank, bad, ar.calls))
+        torch.distributed.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), -1))
+
+
+@pytest.mark.gpu
+def test_ipc_allreduce_two_ranks_one_gpu():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_ipc_ar_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    for rank, bad, calls in res:
+        assert bad == [], bad
+        assert calls > 40
