@@ -112,7 +112,8 @@ def test_tp2_engine_matches_tp1_cpu():
 
 
 @pytest.mark.gpu
-def test_tp2_same_gpu_rehearsal():
+@pytest.mark.parametrize("allreduce", ["auto", "ipc"])
+def test_tp2_same_gpu_rehearsal(allreduce):
     """Two TP ranks on ONE MI355X (gloo control + host-staged collectives, since RCCL
     refuses duplicate devices): exercises the fused decode path's vocab-parallel sampler
     (finalize="key" + MAX all-reduce) and the step-channel protocol on real kernels."""
@@ -123,9 +124,13 @@ def test_tp2_same_gpu_rehearsal():
     exp = [o.token_ids for o in ref_eng.generate(_prompts(), greedy)]
     del ref_eng
     torch.cuda.empty_cache()
-    eng = TPEngine(EngineConfig(tensor_parallel_size=2, tp_same_device=True, **base))
+    eng = TPEngine(EngineConfig(tensor_parallel_size=2, tp_same_device=True,
+                                tp_allreduce=allreduce, **base))
     try:
         got = [o.token_ids for o in eng.generate(_prompts(), greedy)]
+        if allreduce == "ipc":
+            assert eng.comm.ipc is not None and eng.comm.ipc.calls > 0
+            assert eng.comm.ipc.check() == 0
     finally:
         eng.shutdown()
     # bf16 partial sums split across ranks round differently: allow a late near-tie flip
