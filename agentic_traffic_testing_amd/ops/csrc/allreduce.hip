@@ -146,6 +146,9 @@ static int launch(const Params& p, const void* x, void* y, int64_t n, int blocks
 }
 
 }  // namespace ar
+}  // namespace atta
+
+using namespace atta;
 
 size_t atta_ar_buffer_bytes(int64_t max_elems, int elem_bytes) {
   return ar::kHeaderBytes + 2 * ar::kMaxRanks * static_cast<size_t>(max_elems) * elem_bytes;
@@ -191,5 +194,3 @@ int atta_ar_run(void* const* bases, int rank, int world, int64_t max_elems, cons
   return dtype == 0 ? ar::launch<__bf16>(p, x, y, n, ar::kMaxBlocks, stream)
                     : ar::launch<_Float16>(p, x, y, n, ar::kMaxBlocks, stream);
 }
-
-}  // namespace atta

@@ -1,0 +1,31 @@
+"""The in-tree native libraries build for gfx950 and load on a CPU-only host (catches
+undefined symbols / missing registrations before a GPU box ever sees them)."""
+import torch
+
+from agentic_traffic_testing_amd.ops import build
+
+EXPECTED_OPS = {
+    "rms_norm", "fused_add_rms_norm", "silu_and_mul", "rope_cache", "attention_prefill",
+    "attention_decode", "attention_decode_v2", "sample", "skinny_gemm", "fused_qkv_rope",
+    "fused_gate_up_silu", "fused_lm_head_sample", "sample_finalize", "skinny_variant",
+    "ar_buffer_bytes", "ar_alloc", "ar_free", "ar_handle", "ar_open", "ar_close", "ar_error",
+    "ar_run",
+}
+
+
+def test_kernel_library_loads_and_registers_all_ops():
+    so = build.build_kernels()
+    torch.ops.load_library(str(so))
+    for name in EXPECTED_OPS:
+        assert hasattr(torch.ops.atta, name), name
+        getattr(torch.ops.atta, name).default  # schema registered
+    # host-only helper callable without a GPU
+    assert torch.ops.atta.ar_buffer_bytes(1024, 2) == 64 * 1024 + 2 * 8 * 1024 * 2
+
+
+def test_runtime_extension_loads():
+    from agentic_traffic_testing_amd.runtime import BlockManager, ShmChannel
+
+    bm = BlockManager(8, 16, True)
+    assert bm.num_free_blocks() == 8
+    assert ShmChannel is not None
