@@ -162,6 +162,9 @@ class EngineConfig:
     fused_decode: bool = True
     # keep a pre-shuffled copy of the decode-GEMV weights (contiguous 1 KiB wave loads)
     preshuffle_decode_weights: bool = True
+    # "" = 16-bit weights; "fp8" = OCP e4m3fn weight-only quantisation with per-row scales
+    # (decode: fp8 GEMV kernels; prefill: hipBLASLt fp8 GEMM) - BASELINE config 5
+    quantization: str = ""
     num_kv_blocks: int = 0               # 0 = size from gpu_memory_utilization
     load_format: str = "auto"            # auto | dummy (random init) | safetensors
     # tensor parallelism: "auto" = RCCL ("nccl") on GPUs, gloo on CPU; "gloo" forces the
@@ -205,5 +208,7 @@ class EngineConfig:
         n = _env_int("LLM_TENSOR_PARALLEL_SIZE", 0)
         if n > 0:
             kw["tensor_parallel_size"] = n
+        if env.get("LLM_QUANTIZATION"):
+            kw["quantization"] = env["LLM_QUANTIZATION"].strip().lower()
         kw.update({k: v for k, v in overrides.items() if v is not None})
         return cfg.replace(**kw)

@@ -112,12 +112,14 @@ class ModelRunner:
         self.tp_rank, self.tp_size = tp_rank, tp_size
         self.publisher = None     # rank 0 of a TP group: ShmChannel to the workers
         t0 = time.perf_counter()
-        self.model = LlamaModel(model_cfg, self.dtype, self.device, tp_rank, tp_size, comm)
+        self.model = LlamaModel(model_cfg, self.dtype, self.device, tp_rank, tp_size, comm,
+                                quantization=cfg.quantization)
         if weights_dir and cfg.load_format != "dummy":
             self.model.load_safetensors(weights_dir)
         else:
             self.model.init_random(seed=cfg.seed)
-        if self.is_cuda and cfg.fused_decode and cfg.preshuffle_decode_weights:
+        if self.is_cuda and ((cfg.fused_decode and cfg.preshuffle_decode_weights)
+                             or cfg.quantization == "fp8"):
             self.model.prepare_decode_weights()
         self.load_seconds = time.perf_counter() - t0
         self.block_size = cfg.block_size

@@ -67,12 +67,23 @@ class LayerWeights:
     o_ps: torch.Tensor | None = None
     gate_up_ps: torch.Tensor | None = None
     down_ps: torch.Tensor | None = None
+    # fp8 weight-only quantisation (GPU): the projections above are uint8 e4m3fn bytes and
+    # these are their fp32 per-output-row scales
+    qkv_s: torch.Tensor | None = None
+    o_s: torch.Tensor | None = None
+    gate_up_s: torch.Tensor | None = None
+    down_s: torch.Tensor | None = None
 
 
 class LlamaModel:
     def __init__(self, cfg: ModelConfig, dtype=torch.bfloat16, device="cuda", tp_rank: int = 0,
-                 tp_size: int = 1, tp_group=None):
+                 tp_size: int = 1, tp_group=None, quantization: str = ""):
         # tp_group: parallel.comm.TPComm (required when tp_size > 1)
+        # quantization: "" (16-bit weights) | "fp8" (OCP e4m3fn weights, per-row scales; on the
+        # CPU reference path the dequantised values are stored instead)
+        if quantization not in ("", "fp8"):
+            raise ValueError(f"unsupported quantization {quantization!r}")
+        self.quant = quantization
         self.cfg = cfg
         self.dtype = dtype
         self.device = torch.device(device)
@@ -172,7 +183,18 @@ class LlamaModel:
         qkv = (qkv.float() * n_in.float()[None, :]).to(qkv.dtype).contiguous()
         gu = (gu.float() * n_post.float()[None, :]).to(gu.dtype).contiguous()
         ones = self._ones(n_in)
+        if self.quant == "fp8":
+            return self._quantize_layer(ones, qkv, o, gu, down)
         return LayerWeights(ones, qkv, o, ones, gu, down)
+
+    def _quantize_layer(self, ones, qkv, o, gu, down) -> LayerWeights:
+        """fp8 weight-only quantisation of the four projections (after norm folding)."""
+        qs = [ops.quantize_fp8(w) for w in (qkv, o, gu, down)]
+        if self.device.type != "cuda":  # CPU reference: the values fp8 can represent
+            deq = [ops.dequantize_fp8(q, sc, self.dtype) for q, sc in qs]
+            return LayerWeights(ones, deq[0], deq[1], ones, deq[2], deq[3])
+        return LayerWeights(ones, qs[0][0], qs[1][0], ones, qs[2][0], qs[3][0],
+                            qkv_s=qs[0][1], o_s=qs[1][1], gate_up_s=qs[2][1], down_s=qs[3][1])
 
     def _ones(self, like):
         if getattr(self, "_ones_t", None) is None or self._ones_t.shape != like.shape:
@@ -228,6 +250,12 @@ class LlamaModel:
         if self.device.type != "cuda":
             return self
         for L in self.layers:
+            if L.qkv_s is not None:  # fp8: 16-row x 64-col blocks of bytes
+                L.qkv_ps = ops.preshuffle_fp8(L.qkv, "qkv")
+                L.o_ps = ops.preshuffle_fp8(L.o)
+                L.gate_up_ps = ops.preshuffle_fp8(L.gate_up, "silu")
+                L.down_ps = ops.preshuffle_fp8(L.down)
+                continue
             L.qkv_ps = ops.preshuffle(L.qkv, "qkv")
             L.o_ps = ops.preshuffle(L.o)
             L.gate_up_ps = ops.preshuffle(L.gate_up, "silu")
@@ -238,10 +266,23 @@ class LlamaModel:
 
     # ---------------------------------------------------------------------------------
     def weight_bytes(self) -> int:
-        n = self.embed.numel() + self.norm.numel() + self.lm_head.numel()
+        """Bytes of the weights one forward streams (row-major copies, scales included)."""
+        ts = [self.embed, self.norm, self.lm_head]
         for l in self.layers:
-            n += sum(t.numel() for t in (l.input_norm, l.qkv, l.o, l.post_norm, l.gate_up, l.down))
-        return n * self.embed.element_size()
+            ts += [l.input_norm, l.qkv, l.o, l.post_norm, l.gate_up, l.down, l.qkv_s, l.o_s,
+                   l.gate_up_s, l.down_s]
+        return sum(t.numel() * t.element_size() for t in ts if t is not None)
+
+    @staticmethod
+    def _proj(x, w, scale, residual=None):
+        """Prefill / generic projection: fp8 weights go through the fp8 GEMM path."""
+        if scale is None:
+            return ops.linear(x, w, residual=residual)
+        y = ops.linear_fp8(x, w, scale)
+        if residual is not None:
+            residual.copy_((y.float() + residual.float()).to(residual.dtype))
+            return residual
+        return y
 
     def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         if self.tp_size > 1:
@@ -263,7 +304,7 @@ class LlamaModel:
                 x = ops.rms_norm(h, L.input_norm, eps)
             else:
                 x = ops.fused_add_rms_norm(h, residual, L.input_norm, eps)
-            qkv = ops.linear(x, L.qkv)
+            qkv = self._proj(x, L.qkv, L.qkv_s)
             q = ops.rope_cache(qkv, md.positions, md.slot_mapping, self.cos_sin, k_caches[li],
                                v_caches[li], nq, nkv, D)
             attn = torch.empty_like(q)
@@ -275,11 +316,11 @@ class LlamaModel:
                 ops.attention_prefill(q, k_caches[li], v_caches[li], md.block_tables,
                                       md.seq_kvlen, md.seq_qstart, md.tile_seq, md.tile_qoff,
                                       self.scale, out=attn)
-            h = self._all_reduce(ops.linear(attn.view(T, nq * D), L.o))
+            h = self._all_reduce(self._proj(attn.view(T, nq * D), L.o, L.o_s))
             x = ops.fused_add_rms_norm(h, residual, L.post_norm, eps)
-            gu = ops.linear(x, L.gate_up)
+            gu = self._proj(x, L.gate_up, L.gate_up_s)
             a = ops.silu_and_mul(gu)
-            h = self._all_reduce(ops.linear(a, L.down))
+            h = self._all_reduce(self._proj(a, L.down, L.down_s))
         return ops.fused_add_rms_norm(h, residual, self.norm, eps)
 
     def decode_fusable(self, num_tokens: int) -> bool:
@@ -305,9 +346,11 @@ class LlamaModel:
         act = ws["act"][:B]
         for li, L in enumerate(self.layers):
             ps = L.qkv_ps is not None
+            if L.qkv_s is not None and not ps:
+                raise RuntimeError("fp8 decode needs prepare_decode_weights()")
             ops.decode_qkv_rope(residual, L.qkv_ps if ps else L.qkv, eps, md.positions,
                                 md.slot_mapping, self.cos_sin, k_caches[li], v_caches[li], nq, nkv,
-                                q_out=q, preshuffled=ps)
+                                q_out=q, preshuffled=ps, w_scale=L.qkv_s)
             ops.attention_decode_v2(q, k_caches[li], v_caches[li], md.block_tables,
                                     md.seq_kvlen, md.seq_qstart, self.scale, ws["part_out"],
                                     ws["part_lse"], ws["counters"], ws["max_parts"],
@@ -315,18 +358,18 @@ class LlamaModel:
             a2 = attn.view(B, nq * self.head_dim)
             if self.tp_size == 1:
                 ops.linear(a2, L.o_ps if ps else L.o, residual=residual, waves=ops.WAVES_SMALL,
-                           preshuffled=ps)
+                           preshuffled=ps, w_scale=L.o_s)
             else:
                 residual.add_(self._all_reduce(ops.linear(a2, L.o_ps if ps else L.o,
-                                                          preshuffled=ps)))
+                                                          preshuffled=ps, w_scale=L.o_s)))
             ops.decode_gate_up_silu(residual, L.gate_up_ps if ps else L.gate_up, eps, out=act,
-                                    preshuffled=ps)
+                                    preshuffled=ps, w_scale=L.gate_up_s)
             if self.tp_size == 1:
                 ops.linear(act, L.down_ps if ps else L.down, residual=residual,
-                           waves=ops.WAVES_LARGE, preshuffled=ps)
+                           waves=ops.WAVES_LARGE, preshuffled=ps, w_scale=L.down_s)
             else:
                 residual.add_(self._all_reduce(ops.linear(act, L.down_ps if ps else L.down,
-                                                          preshuffled=ps)))
+                                                          preshuffled=ps, w_scale=L.down_s)))
         lm_ps = self.lm_head_ps is not None
         lm = self.lm_head_ps if lm_ps else self.lm_head
         if self.tp_size == 1:

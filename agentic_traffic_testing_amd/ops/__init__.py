@@ -177,27 +177,87 @@ def preshuffle(w: torch.Tensor, rowmap: str = "plain") -> torch.Tensor:
     N, K = w.shape
     if N % 16 or K % 32:
         raise ValueError(f"preshuffle needs N % 16 == 0 and K % 32 == 0, got {tuple(w.shape)}")
-    dev = w.device
+    rows = _rowmap_index(N, rowmap, w.device)
+    if rows is not None:
+        w = w.index_select(0, rows)
+    return (w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+            .reshape(N, K))
+
+
+# ---- fp8 weight-only quantisation (OCP e4m3fn, per output row) ----------------------------
+FP8_MAX = 448.0
+
+
+def quantize_fp8(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """[N, K] 16-bit weight -> (uint8 e4m3fn bytes [N, K], fp32 per-row scale [N])."""
+    wf = w.float()
+    scale = (wf.abs().amax(dim=1) / FP8_MAX).clamp_min(1e-12)
+    q = (wf / scale[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    return q.view(torch.uint8), scale.contiguous()
+
+
+def dequantize_fp8(q: torch.Tensor, scale: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
+    return (q.view(torch.float8_e4m3fn).float() * scale[:, None].float()).to(dtype)
+
+
+def preshuffle_fp8(q: torch.Tensor, rowmap: str = "plain") -> torch.Tensor:
+    """fp8 analogue of ``preshuffle``: rows permuted by ``rowmap``, then each 16-row x 64-col
+    block stored as 64 lanes x 16 bytes, lane l = (row l & 15) holding its 8 k-values of the
+    two 32-wide K steps (k = 8*(l >> 4) + j and 32 + 8*(l >> 4) + j)."""
+    N, K = q.shape
+    if N % 16 or K % 64:
+        raise ValueError(f"fp8 preshuffle needs N % 16 == 0 and K % 64 == 0, got {tuple(q.shape)}")
+    rows = _rowmap_index(N, rowmap, q.device)
+    if rows is not None:
+        q = q.index_select(0, rows)
+    return (q.reshape(N // 16, 16, K // 64, 2, 4, 8).permute(0, 2, 4, 1, 3, 5).contiguous()
+            .reshape(N, K))
+
+
+def _rowmap_index(N: int, rowmap: str, dev):
+    if rowmap == "plain":
+        return None
     if rowmap == "qkv":
         if N % 128:
             raise ValueError("qkv rowmap needs whole 128-dim heads")
         t = torch.arange(N // 16, device=dev)
         c = torch.arange(16, device=dev)
         head, j = (t >> 3)[:, None], (t & 7)[:, None]
-        idx = (head * 128 + j * 8 + (c & 7)[None, :] + ((c & 8) != 0)[None, :] * 64).reshape(-1)
-        w = w.index_select(0, idx)
-    elif rowmap == "silu":
+        return (head * 128 + j * 8 + (c & 7)[None, :] + ((c & 8) != 0)[None, :] * 64).reshape(-1)
+    if rowmap == "silu":
         inter = N // 2
         if inter % 8:
             raise ValueError("silu rowmap needs inter % 8 == 0")
         t = torch.arange(inter // 8, device=dev)[:, None]
         c = torch.arange(16, device=dev)[None, :]
-        idx = torch.where(c < 8, t * 8 + c, inter + t * 8 + c - 8).reshape(-1)
-        w = w.index_select(0, idx)
-    elif rowmap != "plain":
-        raise ValueError(f"unknown rowmap {rowmap}")
-    return (w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
-            .reshape(N, K))
+        return torch.where(c < 8, t * 8 + c, inter + t * 8 + c - 8).reshape(-1)
+    raise ValueError(f"unknown rowmap {rowmap}")
+
+
+_SCALED_MM_OK: bool | None = None
+
+
+def linear_fp8(x: torch.Tensor, q: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    """Prefill-sized y = x @ dequant(q).T with row-major fp8 weights: per-tensor dynamic
+    activation scale, hipBLASLt fp8 GEMM (torch._scaled_mm, fp8 MFMA), per-row weight scale
+    applied to the bf16 output.  Falls back to dequantise + GEMM where _scaled_mm is absent."""
+    global _SCALED_MM_OK
+    if x.is_cuda and _SCALED_MM_OK is not False:
+        try:
+            sx = (x.float().abs().amax() / FP8_MAX).clamp_min(1e-12)
+            xq = (x.float() / sx).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+            one = torch.ones((), device=x.device, dtype=torch.float32)
+            y = torch._scaled_mm(xq, q.view(torch.float8_e4m3fn).t(), scale_a=sx, scale_b=one,
+                                 out_dtype=x.dtype)
+            _SCALED_MM_OK = True
+            return (y.float() * scale[None, :]).to(x.dtype)
+        except (RuntimeError, TypeError) as e:
+            if _SCALED_MM_OK:
+                raise
+            _SCALED_MM_OK = False
+            print(f"[atta] torch._scaled_mm unavailable for fp8 prefill ({e}); "
+                  "dequantising per GEMM", flush=True)
+    return torch.nn.functional.linear(x, dequantize_fp8(q, scale, x.dtype))
 
 
 def _need_cuda(x, preshuffled):
@@ -207,21 +267,25 @@ def _need_cuda(x, preshuffled):
 
 def linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None,
            out: torch.Tensor | None = None, waves: int | None = None,
-           preshuffled: bool = False) -> torch.Tensor:
+           preshuffled: bool = False, w_scale: torch.Tensor | None = None) -> torch.Tensor:
     """y = x @ w.T.  With ``residual`` the product is added to ``residual`` IN PLACE and
     ``residual`` is returned (residual-stream update).  Decode-sized M runs the MFMA skinny
     GEMM; everything else (prefill, CPU) runs F.linear (hipBLASLt on the GPU).
-    ``preshuffled``: ``w`` comes from ``preshuffle`` (skinny path only)."""
-    _need_cuda(x, preshuffled)
+    ``preshuffled``: ``w`` comes from ``preshuffle`` (skinny path only).
+    ``w_scale``: ``w`` is fp8 (uint8, ``preshuffle_fp8`` layout) with this per-row scale."""
+    _need_cuda(x, preshuffled or w_scale is not None)
+    if w_scale is not None:
+        preshuffled = True
     if preshuffled and not skinny_ok(x, w):
         raise ValueError("pre-shuffled weights need the skinny (decode) path")
     if skinny_ok(x, w):
         if residual is not None:
-            _native().skinny_gemm(residual, x, w, residual, waves or SKINNY_WAVES, preshuffled)
+            _native().skinny_gemm(residual, x, w, residual, waves or SKINNY_WAVES, preshuffled,
+                                  w_scale)
             return residual
         if out is None:
             out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
-        _native().skinny_gemm(out, x, w, None, waves or SKINNY_WAVES, preshuffled)
+        _native().skinny_gemm(out, x, w, None, waves or SKINNY_WAVES, preshuffled, w_scale)
         return out
     y = torch.nn.functional.linear(x, w)
     if residual is not None:
@@ -235,9 +299,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = Non
 
 # ---- fused decode-step ops (norm weight folded into W on the host) -----------------------
 def decode_qkv_rope(x, w, eps, positions, slots, cos_sin, k_cache, v_cache, n_q_heads,
-                    n_kv_heads, q_out=None, preshuffled=False):
+                    n_kv_heads, q_out=None, preshuffled=False, w_scale=None):
     """RMSNorm(x) -> QKV GEMM -> RoPE -> q out + paged K/V write, one kernel on the GPU."""
-    _need_cuda(x, preshuffled)
+    _need_cuda(x, preshuffled or w_scale is not None)
     if q_out is None:
         q_out = torch.empty(x.shape[0], n_q_heads, 128, dtype=x.dtype, device=x.device)
     if not x.is_cuda:
@@ -247,13 +311,14 @@ def decode_qkv_rope(x, w, eps, positions, slots, cos_sin, k_cache, v_cache, n_q_
         q_out.copy_(q)
         return q_out
     _native().fused_qkv_rope(q_out, k_cache, v_cache, x, w, positions, slots, cos_sin,
-                             n_q_heads, n_kv_heads, eps, WAVES_SMALL, preshuffled)
+                             n_q_heads, n_kv_heads, eps, WAVES_SMALL,
+                             preshuffled or w_scale is not None, w_scale)
     return q_out
 
 
-def decode_gate_up_silu(x, w, eps, out=None, preshuffled=False):
+def decode_gate_up_silu(x, w, eps, out=None, preshuffled=False, w_scale=None):
     """RMSNorm(x) -> gate_up GEMM -> SiLU(gate) * up, one kernel on the GPU."""
-    _need_cuda(x, preshuffled)
+    _need_cuda(x, preshuffled or w_scale is not None)
     inter = w.shape[0] // 2
     if out is None:
         out = torch.empty(x.shape[0], inter, dtype=x.dtype, device=x.device)
@@ -261,7 +326,8 @@ def decode_gate_up_silu(x, w, eps, out=None, preshuffled=False):
         n = ref.rms_norm(x, torch.ones(x.shape[1], dtype=x.dtype), eps)
         out.copy_(ref.silu_and_mul(torch.nn.functional.linear(n, w)))
         return out
-    _native().fused_gate_up_silu(out, x, w, eps, WAVES_LARGE, preshuffled)
+    _native().fused_gate_up_silu(out, x, w, eps, WAVES_LARGE, preshuffled or w_scale is not None,
+                                 w_scale)
     return out
 
 

@@ -152,20 +152,39 @@ void sample(at::Tensor out, const at::Tensor& logits, const at::Tensor& temperat
            "sample");
 }
 
+// fp8 weight-only quantisation: w is uint8 (OCP e4m3fn bytes, pre-shuffled in 16 x 64 blocks)
+// and w_scale the fp32 per-row dequant scale; returns the scale pointer (nullptr: 16-bit w).
+const float* fp8_scale(const at::Tensor& w, const c10::optional<at::Tensor>& w_scale,
+                       const char* what) {
+  if (!w_scale.has_value() || !w_scale->defined()) {
+    TORCH_CHECK(w.scalar_type() != at::kByte, what, ": uint8 (fp8) weights need w_scale");
+    return nullptr;
+  }
+  TORCH_CHECK(w.scalar_type() == at::kByte, what, ": w_scale given but weights are not fp8 bytes");
+  TORCH_CHECK(w_scale->scalar_type() == at::kFloat && w_scale->is_contiguous() &&
+                  w_scale->numel() == w.size(0) && w_scale->is_cuda(),
+              what, ": w_scale must be fp32 [N] on the GPU");
+  TORCH_CHECK(w.size(1) % 64 == 0, what, ": fp8 weights need K % 64 == 0");
+  return w_scale->data_ptr<float>();
+}
+
 // dtype code for the skinny GEMV entry points; bit 8 flags pre-shuffled weights (kPreshuffled)
 int skinny_dtype(const at::Tensor& x, bool preshuffled) {
   return dtype_code(x) | (preshuffled ? kPreshuffled : 0);
 }
 
 void skinny_gemm(at::Tensor y, const at::Tensor& x, const at::Tensor& w,
-                 const c10::optional<at::Tensor>& residual, int64_t waves, bool preshuffled) {
+                 const c10::optional<at::Tensor>& residual, int64_t waves, bool preshuffled,
+                 const c10::optional<at::Tensor>& w_scale) {
   check_dev(x, "x");
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "skinny_gemm: 2-D operands");
   TORCH_CHECK(x.stride(1) == 1 && y.stride(1) == 1 && w.is_contiguous(), "skinny_gemm: layout");
   TORCH_CHECK(x.size(1) == w.size(1) && y.size(0) == x.size(0) && y.size(1) == w.size(0),
               "skinny_gemm: shapes");
-  TORCH_CHECK(x.scalar_type() == w.scalar_type() && y.scalar_type() == x.scalar_type(),
+  TORCH_CHECK((x.scalar_type() == w.scalar_type() || w.scalar_type() == at::kByte) &&
+                  y.scalar_type() == x.scalar_type(),
               "skinny_gemm: dtypes");
+  const float* ws = fp8_scale(w, w_scale, "skinny_gemm");
   const void* r = nullptr;
   int64_t rs = 0;
   if (residual.has_value() && residual->defined()) {
@@ -175,7 +194,7 @@ void skinny_gemm(at::Tensor y, const at::Tensor& x, const at::Tensor& w,
   }
   const at::DeviceGuard g(x.device());
   check_rc(atta_skinny_gemm(y.data_ptr(), x.data_ptr(), w.data_ptr(), r, x.size(0), w.size(0),
-                            w.size(1), x.stride(0), y.stride(0), rs, waves,
+                            w.size(1), x.stride(0), y.stride(0), rs, waves, ws,
                             skinny_dtype(x, preshuffled), cur_stream()),
            "skinny_gemm");
 }
@@ -185,14 +204,17 @@ void check_skinny(const at::Tensor& x, const at::Tensor& w, const char* what) {
   check_dev(x, "x");
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.is_contiguous(), what,
               ": layout");
-  TORCH_CHECK(x.size(1) == w.size(1) && x.scalar_type() == w.scalar_type(), what, ": shapes");
+  TORCH_CHECK(x.size(1) == w.size(1) &&
+                  (x.scalar_type() == w.scalar_type() || w.scalar_type() == at::kByte),
+              what, ": shapes / dtypes");
 }
 
 void fused_qkv_rope(at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache, const at::Tensor& x,
                     const at::Tensor& w, const at::Tensor& positions, const at::Tensor& slots,
                     const at::Tensor& cos_sin, int64_t n_q_heads, int64_t n_kv_heads, double eps,
-                    int64_t waves, bool preshuffled) {
+                    int64_t waves, bool preshuffled, const c10::optional<at::Tensor>& w_scale) {
   check_skinny(x, w, "fused_qkv_rope");
+  const float* ws = fp8_scale(w, w_scale, "fused_qkv_rope");
   TORCH_CHECK(w.size(0) == (n_q_heads + 2 * n_kv_heads) * 128, "fused_qkv_rope: w rows");
   TORCH_CHECK(positions.scalar_type() == at::kInt && slots.scalar_type() == at::kInt,
               "fused_qkv_rope: int32 positions/slots");
@@ -204,30 +226,34 @@ void fused_qkv_rope(at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache, co
                                x.data_ptr(), w.data_ptr(), positions.data_ptr<int>(),
                                slots.data_ptr<int>(), cos_sin.data_ptr<float>(), x.size(0),
                                x.size(1), x.stride(0), q_out.stride(0), n_q_heads, n_kv_heads,
-                               k_cache.size(2), static_cast<float>(eps), waves,
+                               k_cache.size(2), static_cast<float>(eps), waves, ws,
                                skinny_dtype(x, preshuffled), cur_stream()),
            "fused_qkv_rope");
 }
 
 void fused_gate_up_silu(at::Tensor out, const at::Tensor& x, const at::Tensor& w, double eps,
-                        int64_t waves, bool preshuffled) {
+                        int64_t waves, bool preshuffled,
+                        const c10::optional<at::Tensor>& w_scale) {
   check_skinny(x, w, "fused_gate_up_silu");
+  const float* ws = fp8_scale(w, w_scale, "fused_gate_up_silu");
   TORCH_CHECK(w.size(0) == 2 * out.size(1) && out.size(0) == x.size(0) && out.stride(1) == 1,
               "fused_gate_up_silu: out");
   const at::DeviceGuard g(x.device());
   check_rc(atta_fused_gate_up_silu(out.data_ptr(), x.data_ptr(), w.data_ptr(), x.size(0),
                                    x.size(1), out.size(1), x.stride(0), out.stride(0),
-                                   static_cast<float>(eps), waves, skinny_dtype(x, preshuffled),
-                                   cur_stream()),
+                                   static_cast<float>(eps), waves, ws,
+                                   skinny_dtype(x, preshuffled), cur_stream()),
            "fused_gate_up_silu");
 }
 
 void fused_lm_head_sample(at::Tensor tokens, at::Tensor keys, const at::Tensor& x,
                           const at::Tensor& w, double eps, const at::Tensor& temperature,
                           const at::Tensor& seeds, const at::Tensor& steps, int64_t finalize,
-                          int64_t vocab_offset, int64_t waves, bool preshuffled) {
+                          int64_t vocab_offset, int64_t waves, bool preshuffled,
+                          const c10::optional<at::Tensor>& w_scale) {
   TORCH_CHECK(finalize >= 0 && finalize <= 2, "fused_lm_head_sample: finalize mode 0/1/2");
   check_skinny(x, w, "fused_lm_head_sample");
+  const float* ws = fp8_scale(w, w_scale, "fused_lm_head_sample");
   TORCH_CHECK(tokens.scalar_type() == at::kLong && keys.scalar_type() == at::kLong &&
                   seeds.scalar_type() == at::kLong && steps.scalar_type() == at::kLong &&
                   temperature.scalar_type() == at::kFloat,
@@ -240,7 +266,7 @@ void fused_lm_head_sample(at::Tensor tokens, at::Tensor keys, const at::Tensor& 
                reinterpret_cast<unsigned long long*>(keys.data_ptr<int64_t>()), x.data_ptr(),
                w.data_ptr(), x.size(0), w.size(0), x.size(1), x.stride(0), static_cast<float>(eps),
                temperature.data_ptr<float>(), seeds.data_ptr<int64_t>(), steps.data_ptr<int64_t>(),
-               static_cast<int>(finalize), static_cast<int>(vocab_offset), waves,
+               static_cast<int>(finalize), static_cast<int>(vocab_offset), waves, ws,
                skinny_dtype(x, preshuffled), cur_stream()),
            "fused_lm_head_sample");
 }
@@ -368,16 +394,16 @@ TORCH_LIBRARY(atta, m) {
   m.def(
       "fused_qkv_rope(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor x, "
       "Tensor w, Tensor positions, Tensor slots, Tensor cos_sin, int n_q_heads, int n_kv_heads, "
-      "float eps, int waves, bool preshuffled=False) -> ()");
+      "float eps, int waves, bool preshuffled=False, Tensor? w_scale=None) -> ()");
   m.def("fused_gate_up_silu(Tensor(a!) out, Tensor x, Tensor w, float eps, int waves, "
-        "bool preshuffled=False) -> ()");
+        "bool preshuffled=False, Tensor? w_scale=None) -> ()");
   m.def(
       "fused_lm_head_sample(Tensor(a!) tokens, Tensor(b!) keys, Tensor x, Tensor w, float eps, "
       "Tensor temperature, Tensor seeds, Tensor steps, int finalize, int vocab_offset, "
-      "int waves, bool preshuffled=False) -> ()");
+      "int waves, bool preshuffled=False, Tensor? w_scale=None) -> ()");
   m.def("sample_finalize(Tensor(a!) tokens, Tensor keys, int n_tiles) -> ()");
   m.def("skinny_gemm(Tensor(a!) y, Tensor x, Tensor w, Tensor? residual, int waves, "
-        "bool preshuffled=False) -> ()");
+        "bool preshuffled=False, Tensor? w_scale=None) -> ()");
   m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rms_norm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");

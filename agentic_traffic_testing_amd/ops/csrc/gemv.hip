@@ -69,6 +69,26 @@ struct MfmaK32<_Float16> {
   }
 };
 
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+// fp8 (OCP e4m3fn on gfx950) -> 8 x 16-bit MFMA operand.  v_cvt_pk_f32_fp8 turns two fp8
+// bytes into two floats; the pack to bf16 / fp16 is one v_cvt_pk per pair.
+template <typename T>
+__device__ __forceinline__ typename MfmaK32<T>::frag8 fp8x8_to_frag(uint32_t lo, uint32_t hi) {
+  typename MfmaK32<T>::frag8 f;
+  const uint32_t w[2] = {lo, hi};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const auto a = __builtin_amdgcn_cvt_pk_f32_fp8(static_cast<int>(w[h]), false);
+    const auto b = __builtin_amdgcn_cvt_pk_f32_fp8(static_cast<int>(w[h]), true);
+    f[4 * h + 0] = static_cast<T>(a[0]);
+    f[4 * h + 1] = static_cast<T>(a[1]);
+    f[4 * h + 2] = static_cast<T>(b[0]);
+    f[4 * h + 3] = static_cast<T>(b[1]);
+  }
+  return f;
+}
+
 struct SkinnyParams {
   const uint16_t* x;
   const uint16_t* w;
@@ -90,6 +110,7 @@ struct SkinnyParams {
   int key_stride;
   int vocab_offset;          // first vocab id of this TP rank's LM-head shard
   int ps;                    // weights pre-shuffled into the MFMA lane order (see preshuffle)
+  const float* wscale;       // fp8 weights: per-output-row dequant scale (original row index)
   const float* temperature;
   const int64_t* seeds;
   const int64_t* steps;
@@ -125,8 +146,15 @@ __device__ __forceinline__ int tile_row(int tile, int c, const SkinnyParams& p) 
 // 1 KiB the 64 lanes read - lane l at byte 16*l holds row (l & 15), k 8*(l >> 4)..+7 - so
 // each wave load instruction is one contiguous 1 KiB and a wave streams a contiguous
 // range.  ops.preshuffle builds it once at weight-load time.
-template <typename T, int WAVES, int UNROLL, int MT, int EPI, bool NTL = false, bool PS = false>
+//
+// W8 (fp8 weights, bf16/fp16 activations, weight-only quantisation): always pre-shuffled, in
+// 16-row x 64-column blocks of 1 KiB - lane l's 16 bytes are its 8 k-values of two
+// consecutive 32-wide K steps - converted to 16-bit MFMA operands in registers; the
+// per-row scale multiplies the reduced accumulator.  Halves the weight stream.
+template <typename T, int WAVES, int UNROLL, int MT, int EPI, bool NTL = false, bool PS = false,
+          bool W8 = false>
 __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
+  static_assert(!W8 || (UNROLL % 2 == 0), "fp8 weights load K-step pairs");
   using MF = MfmaK32<T>;
   using frag8 = typename MF::frag8;
   constexpr int R = MT * 16;
@@ -147,6 +175,8 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
          : p.w + static_cast<int64_t>(wrow) * p.K + kbeg + 8 * grp;
   // element offset of K-offset k (a multiple of 32) from wp in either layout
   auto woff = [](int k) { return PS ? k * 16 : k; };
+  const uint8_t* wp8 = reinterpret_cast<const uint8_t*>(p.w) +
+                       (static_cast<int64_t>(tile) * (p.K / 64) + kbeg / 64) * 1024 + lane * 16;
   const uint16_t* xp[MT];
   bool xv[MT];
 #pragma unroll
@@ -165,16 +195,32 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
   const bool norm = p.eps > 0.f;
 
   constexpr int STEP = 32 * UNROLL;
+  constexpr int NRAW = W8 ? UNROLL / 2 : UNROLL;  // 16-byte loads per lane per stage
+  using Raw = u32x4;                                // 16 bytes
   const int nsteps = kw / STEP;
-  auto load_w = [&](frag8 (&f)[UNROLL], int k) {
+  auto load_w = [&](Raw (&f)[NRAW], int k) {
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u)
+    for (int u = 0; u < NRAW; ++u) {
+      const Raw* src = W8 ? reinterpret_cast<const Raw*>(wp8 + (k + 64 * u) * 16)
+                          : reinterpret_cast<const Raw*>(wp + woff(k + 32 * u));
       if constexpr (NTL)
-        f[u] = __builtin_nontemporal_load(reinterpret_cast<const frag8*>(wp + woff(k + 32 * u)));
+        f[u] = __builtin_nontemporal_load(src);
       else
-        f[u] = *reinterpret_cast<const frag8*>(wp + woff(k + 32 * u));
+        f[u] = *src;
+    }
   };
-  auto compute = [&](const frag8 (&f)[UNROLL], int k) {
+  auto wfrag = [&](const Raw (&f)[NRAW], int u) -> frag8 {
+    if constexpr (W8) {
+      const Raw r = f[u >> 1];
+      return (u & 1) ? fp8x8_to_frag<T>(r[2], r[3]) : fp8x8_to_frag<T>(r[0], r[1]);
+    } else {
+      return *reinterpret_cast<const frag8*>(&f[u]);
+    }
+  };
+  auto compute = [&](const Raw (&f)[NRAW], int k) {
+    frag8 wf[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) wf[u] = wfrag(f, u);
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       frag8 xf[UNROLL];
@@ -183,13 +229,13 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
         xf[u] = xv[t] ? *reinterpret_cast<const frag8*>(xp[t] + k + 32 * u) : frag8{};
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
-        acc[t] = MF::mma(xf[u], f[u], acc[t]);
+        acc[t] = MF::mma(xf[u], wf[u], acc[t]);
         if (norm) ss[t] += MF::sq8(xf[u]);
       }
     }
   };
   if (nsteps > 0) {
-    frag8 wa[UNROLL], wb[UNROLL];
+    Raw wa[NRAW], wb[NRAW];
     load_w(wa, 0);
     int s = 0;
     for (; s + 2 <= nsteps; s += 2) {
@@ -200,13 +246,15 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
     }
     if (s < nsteps) compute(wa, s * STEP);
   }
-  for (int k = nsteps * STEP; k < kw; k += 32) {  // tail (K not a multiple of the stage)
-    const frag8 wf = *reinterpret_cast<const frag8*>(wp + woff(k));
+  if constexpr (!W8) {
+    for (int k = nsteps * STEP; k < kw; k += 32) {  // tail (K not a multiple of the stage)
+      const frag8 wf = *reinterpret_cast<const frag8*>(wp + woff(k));
 #pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      const frag8 xf = xv[t] ? *reinterpret_cast<const frag8*>(xp[t] + k) : frag8{};
-      acc[t] = MF::mma(xf, wf, acc[t]);
-      if (norm) ss[t] += MF::sq8(xf);
+      for (int t = 0; t < MT; ++t) {
+        const frag8 xf = xv[t] ? *reinterpret_cast<const frag8*>(xp[t] + k) : frag8{};
+        acc[t] = MF::mma(xf, wf, acc[t]);
+        if (norm) ss[t] += MF::sq8(xf);
+      }
     }
   }
 
@@ -229,12 +277,13 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
     for (int q = 0; q < WAVES; ++q) s += ssq[q][threadIdx.x];
     inv_rms[threadIdx.x] = rsqrtf(s / static_cast<float>(p.K) + p.eps);
   }
-  // sum wave partials into red[0]
+  // sum wave partials into red[0] (fp8 weights: times the row's dequant scale)
   for (int e = threadIdx.x; e < R * 16; e += WAVES * 64) {
     const int m = e >> 4, n = e & 15;
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < WAVES; ++q) s += red[q][m][n];
+    if constexpr (W8) s *= p.wscale[tile_row<EPI>(tile, n, p)];
     red[0][m][n] = s;
   }
   __syncthreads();
@@ -340,6 +389,11 @@ template <int WAVES, int UNROLL, int MT, int EPI>
 static void launch_t(int dtype, dim3 grid, hipStream_t st, const SkinnyParams& p) {
   const bool nt = nt_weights();
   const dim3 blk(WAVES * 64);
+  if (p.wscale != nullptr) {  // fp8 weights (pre-shuffled by construction)
+    if (dtype == 0) skinny_kernel<__bf16, WAVES, UNROLL, MT, EPI, false, true, true><<<grid, blk, 0, st>>>(p);
+    else skinny_kernel<_Float16, WAVES, UNROLL, MT, EPI, false, true, true><<<grid, blk, 0, st>>>(p);
+    return;
+  }
   if (dtype == 0) {
     if (p.ps) skinny_kernel<__bf16, WAVES, UNROLL, MT, EPI, false, true><<<grid, blk, 0, st>>>(p);
     else if (nt) skinny_kernel<__bf16, WAVES, UNROLL, MT, EPI, true><<<grid, blk, 0, st>>>(p);
@@ -369,9 +423,11 @@ static void launch_epi(int dtype, int mt, int waves, dim3 grid, hipStream_t st,
 }
 
 // Largest supported wave count <= requested that divides K into 32-wide MFMA steps.
-static int fit_waves(int waves, int K) {
+// (fp8 weights stream 64-wide K-step pairs: granule 64, and 128 per wave at 4 waves.)
+static int fit_waves(int waves, int K, bool fp8 = false) {
   if (waves != 4 && waves != 8 && waves != 16) waves = 8;
-  while (waves > 4 && K % (32 * waves) != 0) waves >>= 1;
+  const int gran = fp8 ? 64 : 32;
+  while (waves > 4 && K % (gran * waves) != 0) waves >>= 1;
   return waves;
 }
 
@@ -432,13 +488,15 @@ static int skinny_checks(int M, int K, int waves) {
 
 int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual, int M, int N,
                      int K, int64_t x_stride, int64_t y_stride, int64_t res_stride, int waves,
-                     int dtype, hipStream_t stream) {
+                     const float* wscale, int dtype, hipStream_t stream) {
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
-  waves = fit_waves(waves, K);
+  waves = fit_waves(waves, K, wscale != nullptr);
   if (skinny_checks(M, K, waves) || N % 16 != 0) return -1;
   SkinnyParams p{};
   p.ps = ps;
+  p.wscale = wscale;
+  if (wscale != nullptr && (K / waves) % (waves == 4 ? 128 : 64) != 0) return -1;
   p.x = static_cast<const uint16_t*>(x);
   p.w = static_cast<const uint16_t*>(w);
   p.M = M;
@@ -466,16 +524,18 @@ int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual
 int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x, const void* w,
                         const int* positions, const int* slots, const float* cos_sin, int M,
                         int K, int64_t x_stride, int64_t q_stride, int n_q_heads, int n_kv_heads,
-                        int block_size, float eps, int waves, int dtype, hipStream_t stream) {
+                        int block_size, float eps, int waves, const float* wscale, int dtype, hipStream_t stream) {
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
-  waves = fit_waves(waves, K);
+  waves = fit_waves(waves, K, wscale != nullptr);
   if (skinny_checks(M, K, waves)) return -1;
   int shift = 0;
   while ((1 << shift) < block_size) ++shift;
   if ((1 << shift) != block_size) return -1;
   SkinnyParams p{};
   p.ps = ps;
+  p.wscale = wscale;
+  if (wscale != nullptr && (K / waves) % (waves == 4 ? 128 : 64) != 0) return -1;
   p.x = static_cast<const uint16_t*>(x);
   p.w = static_cast<const uint16_t*>(w);
   p.y = static_cast<uint16_t*>(q_out);
@@ -499,14 +559,16 @@ int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x
 }
 
 int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int K, int inter,
-                            int64_t x_stride, int64_t out_stride, float eps, int waves, int dtype,
+                            int64_t x_stride, int64_t out_stride, float eps, int waves, const float* wscale, int dtype,
                             hipStream_t stream) {
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
-  waves = fit_waves(waves, K);
+  waves = fit_waves(waves, K, wscale != nullptr);
   if (skinny_checks(M, K, waves) || inter % 8 != 0) return -1;
   SkinnyParams p{};
   p.ps = ps;
+  p.wscale = wscale;
+  if (wscale != nullptr && (K / waves) % (waves == 4 ? 128 : 64) != 0) return -1;
   p.x = static_cast<const uint16_t*>(x);
   p.w = static_cast<const uint16_t*>(w);
   p.y = static_cast<uint16_t*>(out);
@@ -526,13 +588,15 @@ int atta_fused_lm_head_sample(int64_t* tokens, unsigned long long* keys, const v
                               const void* w, int M, int N, int K, int64_t x_stride, float eps,
                               const float* temperature, const int64_t* seeds,
                               const int64_t* steps, int finalize, int vocab_offset,
-                              int waves, int dtype, hipStream_t stream) {
+                              int waves, const float* wscale, int dtype, hipStream_t stream) {
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
-  waves = fit_waves(waves, K);
+  waves = fit_waves(waves, K, wscale != nullptr);
   if (skinny_checks(M, K, waves) || N % 16 != 0) return -1;
   SkinnyParams p{};
   p.ps = ps;
+  p.wscale = wscale;
+  if (wscale != nullptr && (K / waves) % (waves == 4 ? 128 : 64) != 0) return -1;
   p.x = static_cast<const uint16_t*>(x);
   p.w = static_cast<const uint16_t*>(w);
   p.x_stride = x_stride;

@@ -328,6 +328,8 @@ def build_config(args):
     kw["load_format"] = args.load_format
     if args.device:
         kw["device"] = args.device
+    if getattr(args, "quantization", None):
+        kw["quantization"] = args.quantization
     return EngineConfig.from_env(**kw)
 
 
@@ -395,6 +397,8 @@ def make_parser() -> argparse.ArgumentParser:
     p.add_argument("--max-num-batched-tokens", type=int, default=None)
     p.add_argument("--gpu-memory-utilization", type=float, default=None)
     p.add_argument("--tensor-parallel-size", "--tp-size", type=int, default=None)
+    p.add_argument("--quantization", "-q", default=None, choices=["fp8"],
+                   help="fp8 weight-only quantisation (OCP e4m3fn, per-row scales)")
     p.add_argument("--data-parallel-size", "--dp-size", type=int, default=1,
                    help="engine replicas, one per GPU, behind a router on --port "
                         "(parallel/dp_router.py)")

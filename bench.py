@@ -49,6 +49,8 @@ def main():
     ap.add_argument("--dtype", default="bfloat16")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--quantization", default="", choices=["", "fp8"],
+                    help="fp8 weight-only quantisation (BASELINE config 5); headline is bf16")
     ap.add_argument("--parallel", choices=["dp", "tp"], default="dp",
                     help="dp: one engine replica per GPU (default); tp: one engine over all GPUs")
     a = ap.parse_args()
@@ -76,7 +78,8 @@ def main():
                        max_num_seqs=a.max_num_seqs,
                        max_num_batched_tokens=a.max_num_batched_tokens,
                        gpu_memory_utilization=a.gpu_memory_utilization,
-                       use_graphs=not a.no_graphs, seed=1234, device=dev)
+                       use_graphs=not a.no_graphs, seed=1234, device=dev,
+                       quantization=a.quantization)
     t0 = time.perf_counter()
     eng = LLMEngine(cfg)
     eng.runner.capture_all()
@@ -141,6 +144,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16" if "bf" in a.dtype else a.dtype,
+            "weights": a.quantization or "bf16",
             "data": "synthetic (agent fan-out prompts, synthetic tokenizer, seeded random-init "
                     "Llama-3.1-8B weights)",
             "config": {
@@ -179,7 +183,7 @@ def main_tp(a):
                        max_num_batched_tokens=a.max_num_batched_tokens,
                        gpu_memory_utilization=a.gpu_memory_utilization,
                        use_graphs=not a.no_graphs, seed=1234, device="cuda",
-                       tensor_parallel_size=world)
+                       tensor_parallel_size=world, quantization=a.quantization)
     port = int(os.environ.get("MASTER_PORT", "29511"))
     if rank > 0:
         from agentic_traffic_testing_amd.parallel.tp_engine import run_worker

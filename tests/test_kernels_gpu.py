@@ -393,3 +393,61 @@ def test_preshuffled_decode_kernels_bit_identical(m):
     t2 = ops.decode_lm_head_sample(x, ops.preshuffle(wl), 1e-5, temp, seeds, steps, keys,
                                    preshuffled=True)
     assert torch.equal(t1, t2)
+
+
+@pytest.mark.parametrize("m", [1, 5, 20])
+def test_fp8_decode_kernels(m):
+    """fp8 weight-only GEMVs (uint8 e4m3fn, per-row scale, pre-shuffled) against the same
+    kernels on the dequantised 16-bit weights."""
+    torch.manual_seed(31)
+    dt, H = torch.bfloat16, 1024
+    x = torch.randn(m, H, dtype=dt, device="cuda")
+
+    def q(w, rowmap="plain"):
+        qw, sc = ops.quantize_fp8(w)
+        return ops.preshuffle_fp8(qw, rowmap), sc, ops.dequantize_fp8(qw, sc, dt)
+
+    w = torch.randn(2048, H, dtype=dt, device="cuda") * 0.05
+    wq, sc, wd = q(w)
+    close(ops.linear(x, wq, w_scale=sc), ops.linear(x, wd), 2e-2, 2e-2)
+    r1 = torch.randn(m, 2048, dtype=dt, device="cuda")
+    r2 = r1.clone()
+    ops.linear(x, wq, residual=r1, w_scale=sc)
+    ops.linear(x, wd, residual=r2)
+    close(r1, r2, 3e-2, 2e-2)
+    inter = 512
+    wg = torch.randn(2 * inter, H, dtype=dt, device="cuda") * 0.05
+    gq, gs, gd = q(wg, "silu")
+    close(ops.decode_gate_up_silu(x, gq, 1e-5, w_scale=gs), ops.decode_gate_up_silu(x, gd, 1e-5),
+          3e-2, 3e-2)
+    hq, hkv, bs, nb = 8, 2, 16, 8
+    wqkv = torch.randn((hq + 2 * hkv) * 128, H, dtype=dt, device="cuda") * 0.05
+    kq, ks, kd = q(wqkv, "qkv")
+    kc1 = torch.zeros(nb, hkv, bs, 128, dtype=dt, device="cuda")
+    vc1 = torch.zeros(nb, hkv, 128, bs, dtype=dt, device="cuda")
+    kc2, vc2 = kc1.clone(), vc1.clone()
+    pos = torch.arange(m, dtype=torch.int32, device="cuda")
+    slots = torch.arange(m, dtype=torch.int32, device="cuda")
+    cs = ref.rope_cos_sin(128, 64, 500000.0, None, device="cuda")
+    q1 = ops.decode_qkv_rope(x, kq, 1e-5, pos, slots, cs, kc1, vc1, hq, hkv, w_scale=ks)
+    q2 = ops.decode_qkv_rope(x, kd, 1e-5, pos, slots, cs, kc2, vc2, hq, hkv)
+    close(q1, q2, 3e-2, 3e-2)
+    close(kc1, kc2, 3e-2, 3e-2)
+    close(vc1, vc2, 3e-2, 3e-2)
+    # down-proj shape with K not a multiple of 1024 (fp8 wave fitting)
+    wd2 = torch.randn(256, 3584, dtype=dt, device="cuda") * 0.05
+    a = torch.randn(m, 3584, dtype=dt, device="cuda")
+    dq, dsc, dd = q(wd2)
+    close(ops.linear(a, dq, w_scale=dsc), ops.linear(a, dd), 3e-2, 2e-2)
+
+
+def test_fp8_prefill_linear():
+    torch.manual_seed(32)
+    x = torch.randn(300, 1024, dtype=torch.bfloat16, device="cuda")
+    w = torch.randn(512, 1024, dtype=torch.bfloat16, device="cuda") * 0.05
+    qw, sc = ops.quantize_fp8(w)
+    got = ops.linear_fp8(x, qw, sc)
+    exp = torch.nn.functional.linear(x.float(), ops.dequantize_fp8(qw, sc, torch.float32))
+    # activation fp8 rounding dominates: relative error of a few percent of the row scale
+    err = (got.float() - exp).abs().max() / exp.abs().max()
+    assert float(err) < 0.08
