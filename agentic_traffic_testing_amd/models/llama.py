@@ -324,7 +324,8 @@ class LlamaModel:
         return ops.fused_add_rms_norm(h, residual, self.norm, eps)
 
     def decode_fusable(self, num_tokens: int) -> bool:
-        step = 128
+        # 16-bit GEMVs: K % 128 (4 waves x 32); fp8 GEMVs: K % 256 (4 waves x 64)
+        step = 256 if self.quant == "fp8" else 128
         return (self.device.type == "cuda" and num_tokens <= ops.SKINNY_MAX_M
                 and self.cfg.hidden_size % step == 0 and self.inter % step == 0
                 and (self.n_heads * self.head_dim) % step == 0)

@@ -246,7 +246,21 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
     }
     if (s < nsteps) compute(wa, s * STEP);
   }
-  if constexpr (!W8) {
+  if constexpr (W8) {
+    for (int k = nsteps * STEP; k < kw; k += 64) {  // tail: one 64-wide K-step pair at a time
+      const Raw r = *reinterpret_cast<const Raw*>(wp8 + k * 16);
+      const frag8 w0 = fp8x8_to_frag<T>(r[0], r[1]);
+      const frag8 w1 = fp8x8_to_frag<T>(r[2], r[3]);
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const frag8 x0 = xv[t] ? *reinterpret_cast<const frag8*>(xp[t] + k) : frag8{};
+        const frag8 x1 = xv[t] ? *reinterpret_cast<const frag8*>(xp[t] + k + 32) : frag8{};
+        acc[t] = MF::mma(x0, w0, acc[t]);
+        acc[t] = MF::mma(x1, w1, acc[t]);
+        if (norm) ss[t] += MF::sq8(x0) + MF::sq8(x1);
+      }
+    }
+  } else {
     for (int k = nsteps * STEP; k < kw; k += 32) {  // tail (K not a multiple of the stage)
       const frag8 wf = *reinterpret_cast<const frag8*>(wp + woff(k));
 #pragma unroll
@@ -496,7 +510,7 @@ int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual
   SkinnyParams p{};
   p.ps = ps;
   p.wscale = wscale;
-  if (wscale != nullptr && (K / waves) % (waves == 4 ? 128 : 64) != 0) return -1;
+  if (wscale != nullptr && (K / waves) % 64 != 0) return -1;
   p.x = static_cast<const uint16_t*>(x);
   p.w = static_cast<const uint16_t*>(w);
   p.M = M;
@@ -535,7 +549,7 @@ int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x
   SkinnyParams p{};
   p.ps = ps;
   p.wscale = wscale;
-  if (wscale != nullptr && (K / waves) % (waves == 4 ? 128 : 64) != 0) return -1;
+  if (wscale != nullptr && (K / waves) % 64 != 0) return -1;
   p.x = static_cast<const uint16_t*>(x);
   p.w = static_cast<const uint16_t*>(w);
   p.y = static_cast<uint16_t*>(q_out);
@@ -568,7 +582,7 @@ int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int 
   SkinnyParams p{};
   p.ps = ps;
   p.wscale = wscale;
-  if (wscale != nullptr && (K / waves) % (waves == 4 ? 128 : 64) != 0) return -1;
+  if (wscale != nullptr && (K / waves) % 64 != 0) return -1;
   p.x = static_cast<const uint16_t*>(x);
   p.w = static_cast<const uint16_t*>(w);
   p.y = static_cast<uint16_t*>(out);
@@ -596,7 +610,7 @@ int atta_fused_lm_head_sample(int64_t* tokens, unsigned long long* keys, const v
   SkinnyParams p{};
   p.ps = ps;
   p.wscale = wscale;
-  if (wscale != nullptr && (K / waves) % (waves == 4 ? 128 : 64) != 0) return -1;
+  if (wscale != nullptr && (K / waves) % 64 != 0) return -1;
   p.x = static_cast<const uint16_t*>(x);
   p.w = static_cast<const uint16_t*>(w);
   p.x_stride = x_stride;
