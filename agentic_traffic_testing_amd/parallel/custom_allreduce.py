@@ -26,7 +26,9 @@ class IpcAllReduce:
         self.device = torch.device(device)
         self.elem = torch.finfo(dtype).bits // 8
         self.max_elems = max(8, (max_bytes // self.elem + 7) // 8 * 8)
-        ops = torch.ops.atta
+        from ..ops import _native
+
+        ops = self._ops = _native()  # loads the kernel library (fails loudly if absent)
         nbytes = ops.ar_buffer_bytes(self.max_elems, self.elem)
         self.local = ops.ar_alloc(nbytes, self.device.index or 0)
         handle = ops.ar_handle(self.local).tolist()
@@ -49,16 +51,16 @@ class IpcAllReduce:
                 and 0 < x.numel() <= self.max_elems)
 
     def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
-        torch.ops.atta.ar_run(x, x, self.bases, self.comm.rank, self.max_elems)
+        self._ops.ar_run(x, x, self.bases, self.comm.rank, self.max_elems)
         self.calls += 1
         return x
 
     def check(self) -> int:
         """Error word of the local buffer: bit q set = a wait for rank q timed out."""
-        return int(torch.ops.atta.ar_error(self.local))
+        return int(self._ops.ar_error(self.local))
 
     def close(self):
-        ops = torch.ops.atta
+        ops = self._ops
         for p in self.opened:
             ops.ar_close(p)
         self.opened = []
