@@ -403,9 +403,12 @@ template <int WAVES, int UNROLL, int MT, int EPI>
 static void launch_t(int dtype, dim3 grid, hipStream_t st, const SkinnyParams& p) {
   const bool nt = nt_weights();
   const dim3 blk(WAVES * 64);
-  if (p.wscale != nullptr) {  // fp8 weights (pre-shuffled by construction)
-    if (dtype == 0) skinny_kernel<__bf16, WAVES, UNROLL, MT, EPI, false, true, true><<<grid, blk, 0, st>>>(p);
-    else skinny_kernel<_Float16, WAVES, UNROLL, MT, EPI, false, true, true><<<grid, blk, 0, st>>>(p);
+  if (p.wscale != nullptr) {
+    // fp8 weights (pre-shuffled by construction): a 16-byte lane load carries two K steps,
+    // so the stage is twice as deep to keep the same bytes in flight per wave
+    constexpr int U8 = UNROLL * 2;
+    if (dtype == 0) skinny_kernel<__bf16, WAVES, U8, MT, EPI, false, true, true><<<grid, blk, 0, st>>>(p);
+    else skinny_kernel<_Float16, WAVES, U8, MT, EPI, false, true, true><<<grid, blk, 0, st>>>(p);
     return;
   }
   if (dtype == 0) {

@@ -73,6 +73,41 @@ def gemm_sweep():
             print(row, flush=True)
 
 
+def fp8_sweep():
+    """Production GEMV path (ops.linear): pre-shuffled bf16 vs fp8 weights, cold caches."""
+    print("== decode GEMV: bf16-ps vs fp8 (us / weight GB/s), waves 8 and 16")
+    print(f"{'shape':>8} {'M':>3} {'bf16 w8':>13} {'bf16 w16':>13} {'fp8 w8':>13} {'fp8 w16':>13}")
+    for name, n, k in SHAPES:
+        nb16 = n * k * 2
+        ncopy = max(4, math.ceil(768e6 / nb16))
+        ws = [ops.preshuffle(torch.randn(n, k, dtype=torch.bfloat16, device="cuda") * 0.02)
+              for _ in range(ncopy)]
+        qs = []
+        for w in ws:
+            q, sc = ops.quantize_fp8(w)  # layout irrelevant for timing
+            qs.append((ops.preshuffle_fp8(q), sc))
+        for m in (1, 5):
+            x = torch.randn(m, k, dtype=torch.bfloat16, device="cuda")
+            out = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+            row = f"{name:>8} {m:3d}"
+            for fp8 in (False, True):
+                for waves in (8, 16):
+                    i = [0]
+
+                    def f(fp8=fp8, waves=waves):
+                        i[0] = (i[0] + 1) % ncopy
+                        if fp8:
+                            ops.linear(x, qs[i[0]][0], out=out, waves=waves, w_scale=qs[i[0]][1])
+                        else:
+                            ops.linear(x, ws[i[0]], out=out, waves=waves, preshuffled=True)
+                    t = timeit(f)
+                    nbytes = nb16 // 2 if fp8 else nb16
+                    row += f" {t:7.1f}/{nbytes / t / 1e3:5.0f}"
+            print(row, flush=True)
+        del ws, qs
+        torch.cuda.empty_cache()
+
+
 def attn_sweep():
     print("== decode attention (us): v1 = kernel + combine, v2 = in-kernel combine")
     hq, hkv, bs = 32, 8, 16
@@ -109,3 +144,5 @@ if __name__ == "__main__":
         gemm_sweep()
     if what in ("all", "attn"):
         attn_sweep()
+    if what in ("all", "fp8"):
+        fp8_sweep()
