@@ -326,7 +326,9 @@ def decode_gate_up_silu(x, w, eps, out=None, preshuffled=False, w_scale=None):
         n = ref.rms_norm(x, torch.ones(x.shape[1], dtype=x.dtype), eps)
         out.copy_(ref.silu_and_mul(torch.nn.functional.linear(n, w)))
         return out
-    _native().fused_gate_up_silu(out, x, w, eps, WAVES_LARGE, preshuffled or w_scale is not None,
+    # fp8 weights stream best from 8-wave workgroups here (profiles/r1_microbench_v6_fp8.txt)
+    waves = WAVES_SMALL if w_scale is not None else WAVES_LARGE
+    _native().fused_gate_up_silu(out, x, w, eps, waves, preshuffled or w_scale is not None,
                                  w_scale)
     return out
 
