@@ -358,7 +358,8 @@ class LlamaModel:
                                     ws["part_tokens"], out=attn, num_seqs=B)
             a2 = attn.view(B, nq * self.head_dim)
             if self.tp_size == 1:
-                ops.linear(a2, L.o_ps if ps else L.o, residual=residual, waves=ops.WAVES_SMALL,
+                ops.linear(a2, L.o_ps if ps else L.o, residual=residual,
+                           waves=ops.decode_waves("o", ps, L.o_s is not None),
                            preshuffled=ps, w_scale=L.o_s)
             else:
                 residual.add_(self._all_reduce(ops.linear(a2, L.o_ps if ps else L.o,
@@ -367,7 +368,8 @@ class LlamaModel:
                                     preshuffled=ps, w_scale=L.gate_up_s)
             if self.tp_size == 1:
                 ops.linear(act, L.down_ps if ps else L.down, residual=residual,
-                           waves=ops.WAVES_LARGE, preshuffled=ps, w_scale=L.down_s)
+                           waves=ops.decode_waves("down", ps, L.down_s is not None),
+                           preshuffled=ps, w_scale=L.down_s)
             else:
                 residual.add_(self._all_reduce(ops.linear(act, L.down_ps if ps else L.down,
                                                           preshuffled=ps, w_scale=L.down_s)))

@@ -161,6 +161,21 @@ SKINNY_WAVES = int(os.environ.get("ATTA_SKINNY_WAVES", "8"))
 WAVES_SMALL = int(os.environ.get("ATTA_WAVES_SMALL", "8"))
 WAVES_LARGE = int(os.environ.get("ATTA_WAVES_LARGE", "16"))
 
+# Workgroup waves per decode projection and weight format, from cold-cache sweeps on MI355X
+# (profiles/r1_microbench_v5_cold_preshuffle.txt, r1_microbench_v6_fp8.txt, and the
+# pre-shuffled unroll sweep): "rm" row-major 16-bit, "ps" pre-shuffled 16-bit, "fp8".
+DECODE_WAVES = {
+    "qkv": {"rm": 8, "ps": 4, "fp8": 8},
+    "o": {"rm": 8, "ps": 8, "fp8": 8},
+    "gate_up": {"rm": 16, "ps": 16, "fp8": 8},
+    "down": {"rm": 16, "ps": 8, "fp8": 16},
+    "lm_head": {"rm": 16, "ps": 16, "fp8": 16},
+}
+
+
+def decode_waves(proj: str, preshuffled: bool = False, fp8: bool = False) -> int:
+    return DECODE_WAVES[proj]["fp8" if fp8 else ("ps" if preshuffled else "rm")]
+
 
 def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
     m, k = x.shape
@@ -311,7 +326,8 @@ def decode_qkv_rope(x, w, eps, positions, slots, cos_sin, k_cache, v_cache, n_q_
         q_out.copy_(q)
         return q_out
     _native().fused_qkv_rope(q_out, k_cache, v_cache, x, w, positions, slots, cos_sin,
-                             n_q_heads, n_kv_heads, eps, WAVES_SMALL,
+                             n_q_heads, n_kv_heads, eps,
+                             decode_waves("qkv", preshuffled, w_scale is not None),
                              preshuffled or w_scale is not None, w_scale)
     return q_out
 
@@ -326,8 +342,7 @@ def decode_gate_up_silu(x, w, eps, out=None, preshuffled=False, w_scale=None):
         n = ref.rms_norm(x, torch.ones(x.shape[1], dtype=x.dtype), eps)
         out.copy_(ref.silu_and_mul(torch.nn.functional.linear(n, w)))
         return out
-    # fp8 weights stream best from 8-wave workgroups here (profiles/r1_microbench_v6_fp8.txt)
-    waves = WAVES_SMALL if w_scale is not None else WAVES_LARGE
+    waves = decode_waves("gate_up", preshuffled, w_scale is not None)
     _native().fused_gate_up_silu(out, x, w, eps, waves, preshuffled or w_scale is not None,
                                  w_scale)
     return out
@@ -355,7 +370,8 @@ def decode_lm_head_sample(x, w, eps, temperature, seeds, steps, keys, tokens=Non
         return tokens
     mode = 2 if finalize == "key" else (1 if finalize else 0)
     _native().fused_lm_head_sample(tokens, keys, x, w, eps, temperature, seeds, steps, mode,
-                                   vocab_offset, WAVES_LARGE, preshuffled)
+                                   vocab_offset, decode_waves("lm_head", preshuffled),
+                                   preshuffled)
     return tokens
 
 

@@ -425,11 +425,17 @@ static void launch_t(int dtype, dim3 grid, hipStream_t st, const SkinnyParams& p
 template <int EPI>
 static void launch_epi(int dtype, int mt, int waves, dim3 grid, hipStream_t st,
                        const SkinnyParams& p) {
-  // (waves, unroll) picked from the on-device sweep (profiles/r1_microbench_*):
-  // 8 waves x 2-deep stages for the small projections, 16 x 2 for gate_up / down / lm_head.
+  // (waves, unroll) picked from cold-cache on-device sweeps (profiles/r1_microbench_*):
+  // row-major 16-bit weights: 8 x 2 for the small projections, 16 x 2 for the large ones;
+  // pre-shuffled 16-bit weights: 8 waves stream best with 4-deep stages (o, down), 16 x 2
+  // (gate_up, lm_head), 4 x 4 (qkv).  fp8 doubles the depth inside launch_t.
+  const bool ps16 = p.ps && p.wscale == nullptr;
   if (waves == 16) {
     if (mt == 1) launch_t<16, 2, 1, EPI>(dtype, grid, st, p);
     else launch_t<16, 2, 2, EPI>(dtype, grid, st, p);
+  } else if (waves == 8 && ps16) {
+    if (mt == 1) launch_t<8, 4, 1, EPI>(dtype, grid, st, p);
+    else launch_t<8, 4, 2, EPI>(dtype, grid, st, p);
   } else if (waves == 8) {
     if (mt == 1) launch_t<8, 2, 1, EPI>(dtype, grid, st, p);
     else launch_t<8, 2, 2, EPI>(dtype, grid, st, p);
@@ -650,8 +656,8 @@ int atta_skinny_variant(void* y, const void* x, const void* w, int M, int N, int
   p.K = K;
   if (M < 1 || M > 16 || N % 16) return -1;
   dim3 grid(N / 16);
-  static const int waves_of[10] = {8, 8, 4, 4, 8, 16, 8, 16, 8, 16};
-  if (variant < 0 || variant > 9 || K % (32 * waves_of[variant])) return -1;
+  static const int waves_of[14] = {8, 8, 4, 4, 8, 16, 8, 16, 8, 16, 8, 16, 4, 4};
+  if (variant < 0 || variant > 13 || K % (32 * waves_of[variant])) return -1;
   switch (variant) {
     case 0: skinny_kernel<__bf16, 8, 4, 1, EPI_PLAIN, true><<<grid, 512, 0, stream>>>(p); break;
     case 1: skinny_kernel<__bf16, 8, 8, 1, EPI_PLAIN, false><<<grid, 512, 0, stream>>>(p); break;
@@ -664,6 +670,10 @@ int atta_skinny_variant(void* y, const void* x, const void* w, int M, int N, int
     // 8 / 9: pre-shuffled weights (w must come from ops.preshuffle)
     case 8: skinny_kernel<__bf16, 8, 2, 1, EPI_PLAIN, false, true><<<grid, 512, 0, stream>>>(p); break;
     case 9: skinny_kernel<__bf16, 16, 2, 1, EPI_PLAIN, false, true><<<grid, 1024, 0, stream>>>(p); break;
+    case 10: skinny_kernel<__bf16, 8, 4, 1, EPI_PLAIN, false, true><<<grid, 512, 0, stream>>>(p); break;
+    case 11: skinny_kernel<__bf16, 16, 4, 1, EPI_PLAIN, false, true><<<grid, 1024, 0, stream>>>(p); break;
+    case 12: skinny_kernel<__bf16, 4, 4, 1, EPI_PLAIN, false, true><<<grid, 256, 0, stream>>>(p); break;
+    case 13: skinny_kernel<__bf16, 4, 8, 1, EPI_PLAIN, false, true><<<grid, 256, 0, stream>>>(p); break;
     default: return -1;
   }
   return static_cast<int>(hipGetLastError());

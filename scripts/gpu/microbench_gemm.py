@@ -20,8 +20,10 @@ from agentic_traffic_testing_amd import ops  # noqa: E402
 SHAPES = [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096),
           ("down", 4096, 14336), ("lm_head", 128256, 4096)]
 VARIANTS = {0: "w8u4-nt", 1: "w8u8", 2: "w4u4", 3: "w4u8", 4: "w8u4", 5: "w16u4",
-            6: "w8u2", 7: "w16u2", 8: "w8u2-ps", 9: "w16u2-ps"}
-PRESHUFFLED = {8, 9}
+            6: "w8u2", 7: "w16u2", 8: "w8u2-ps", 9: "w16u2-ps", 10: "w8u4-ps",
+            11: "w16u4-ps", 12: "w4u4-ps", 13: "w4u8-ps"}
+PRESHUFFLED = {8, 9, 10, 11, 12, 13}
+SWEEP = os.environ.get("MB_VARIANTS")  # e.g. "6,7,8,9,10,11,12,13"
 
 
 def timeit(fn, iters=40, reps=3):
@@ -42,7 +44,8 @@ def timeit(fn, iters=40, reps=3):
 
 def gemm_sweep():
     print("== skinny GEMM (us / GB/s)")
-    hdr = f"{'shape':>8} {'M':>3} {'blaslt':>13}" + "".join(f" {v:>15}" for v in VARIANTS.values())
+    hdr = f"{'shape':>8} {'M':>3} {'blaslt':>13}" + "".join(
+        f" {v:>15}" for k, v in VARIANTS.items() if not SWEEP or str(k) in SWEEP.split(","))
     print(hdr)
     for name, n, k in SHAPES:
         nbytes = n * k * 2
@@ -61,6 +64,8 @@ def gemm_sweep():
             tb = timeit(blas)
             row = f"{name:>8} {m:3d} {tb:7.1f}/{nbytes / tb / 1e3:5.0f}"
             for vid in VARIANTS:
+                if SWEEP and str(vid) not in SWEEP.split(","):
+                    continue
                 def f(vid=vid):
                     i[0] = (i[0] + 1) % ncopy
                     src = wps if vid in PRESHUFFLED else ws

@@ -347,9 +347,13 @@ def test_attention_decode_v2(hq, hkv, part_tokens):
 
 
 @pytest.mark.parametrize("m", [1, 5, 20])
-def test_preshuffled_decode_kernels_bit_identical(m):
+def test_preshuffled_decode_kernels_bit_identical(m, monkeypatch):
     """Pre-shuffled weights feed the same lanes the same products in the same order, so every
-    fused decode kernel must return bit-identical results to the row-major layout."""
+    fused decode kernel must return bit-identical results to the row-major layout (at the same
+    wave count: the tuned table may split K differently per layout)."""
+    monkeypatch.setattr(ops, "DECODE_WAVES",
+                        {k: {"rm": v["rm"], "ps": v["rm"], "fp8": v["fp8"]}
+                         for k, v in ops.DECODE_WAVES.items()})
     torch.manual_seed(21)
     dt, H, bs = torch.bfloat16, 1024, 16
     x = torch.randn(m, H, dtype=dt, device="cuda")
