@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(kThreads) oneshot_kernel(Params p, const uint1
     // bounded wait (~2-4 s): a dead peer must not hang the GPU; the block then records the
     // failure in the error word and finishes (the result is garbage, the host checks it)
     uint32_t spins = 0;
-    while (static_cast<int32_t>(__hip_atomic_load(f, __ATOMIC_ACQUIRE,
+    while (static_cast<int32_t>(__hip_atomic_load(f, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_SYSTEM) - gen) < 0) {
       __builtin_amdgcn_s_sleep(2);
       if (++spins > (1u << 25)) {
@@ -99,6 +99,7 @@ __global__ void __launch_bounds__(kThreads) oneshot_kernel(Params p, const uint1
         break;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, once after the poll
   }
   __syncthreads();
   // 4) reduce the W slots in rank order (fp32) into y

@@ -20,6 +20,26 @@ typedef __attribute__((ext_vector_type(4))) short i16x4;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+// fp8 (OCP e4m3fn on gfx950) -> 8 x 16-bit MFMA operand V (bf16x8 / f16x8).
+// v_cvt_pk_f32_fp8 turns two fp8 bytes into two floats; the pack to 16 bits is one
+// v_cvt_pk per pair.
+template <typename T, typename V>
+__device__ __forceinline__ V fp8x8_cvt(uint32_t lo, uint32_t hi) {
+  V f;
+  const uint32_t w[2] = {lo, hi};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const auto a = __builtin_amdgcn_cvt_pk_f32_fp8(static_cast<int>(w[h]), false);
+    const auto b = __builtin_amdgcn_cvt_pk_f32_fp8(static_cast<int>(w[h]), true);
+    f[4 * h + 0] = static_cast<T>(a[0]);
+    f[4 * h + 1] = static_cast<T>(a[1]);
+    f[4 * h + 2] = static_cast<T>(b[0]);
+    f[4 * h + 3] = static_cast<T>(b[1]);
+  }
+  return f;
+}
 
 // 16-byte packet of eight 16-bit values.
 struct alignas(16) Pack8 {
@@ -51,6 +71,33 @@ __device__ __forceinline__ uint16_t from_f32<__bf16>(float f) {
 template <>
 __device__ __forceinline__ uint16_t from_f32<_Float16>(float f) {
   return __builtin_bit_cast(uint16_t, static_cast<_Float16>(f));
+}
+
+// ---- device-coherent hand-over between workgroups -------------------------------------
+// MI355X has one L2 per XCD and the L2s are not coherent with each other, so data one
+// workgroup hands to another inside a launch normally needs an agent-scope release/acquire
+// pair - which on gfx950 writes back / invalidates the WHOLE L2 of the XCD (buffer_wbl2 sc1 /
+// buffer_inv sc1): measured 2.5 us (ctx 1000) to 8 us (ctx 2000) per decode-attention
+// launch.  Instead the handed-over data is stored and loaded with device scope (sc1 cache
+// policy: written through / missed in the XCD L2) through buffer instructions, which needs
+// no fence: a device-scope store is visible device-wide once its vmcnt ack is back, and a
+// device-scope load never returns a stale L1/L2 line.  Byte offsets are 32-bit.
+constexpr int kScDevice = 16;  // aux cache-policy bits: sc1 (scope = device)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dev_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7FFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ void dev_store16(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kScDevice);
+}
+__device__ __forceinline__ u32x4 dev_load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kScDevice);
+}
+__device__ __forceinline__ void dev_store4(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, kScDevice);
+}
+__device__ __forceinline__ float dev_load4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, kScDevice));
 }
 
 // ---- wave / block reductions -----------------------------------------------------------

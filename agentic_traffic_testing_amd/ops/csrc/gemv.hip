@@ -69,24 +69,9 @@ struct MfmaK32<_Float16> {
   }
 };
 
-typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
-
-// fp8 (OCP e4m3fn on gfx950) -> 8 x 16-bit MFMA operand.  v_cvt_pk_f32_fp8 turns two fp8
-// bytes into two floats; the pack to bf16 / fp16 is one v_cvt_pk per pair.
 template <typename T>
 __device__ __forceinline__ typename MfmaK32<T>::frag8 fp8x8_to_frag(uint32_t lo, uint32_t hi) {
-  typename MfmaK32<T>::frag8 f;
-  const uint32_t w[2] = {lo, hi};
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const auto a = __builtin_amdgcn_cvt_pk_f32_fp8(static_cast<int>(w[h]), false);
-    const auto b = __builtin_amdgcn_cvt_pk_f32_fp8(static_cast<int>(w[h]), true);
-    f[4 * h + 0] = static_cast<T>(a[0]);
-    f[4 * h + 1] = static_cast<T>(a[1]);
-    f[4 * h + 2] = static_cast<T>(b[0]);
-    f[4 * h + 3] = static_cast<T>(b[1]);
-  }
-  return f;
+  return fp8x8_cvt<T, typename MfmaK32<T>::frag8>(lo, hi);
 }
 
 struct SkinnyParams {

@@ -34,6 +34,23 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 METRIC = "llm-backend tokens/sec + p50 TTFT under 5-agent fan-out, Llama-3-8B TP=1"
 
 
+
+def overrides(items: list[str]) -> dict:
+    """--set key=value pairs -> EngineConfig kwargs, typed like the field's default."""
+    from dataclasses import fields
+
+    from agentic_traffic_testing_amd.config import EngineConfig
+
+    types = {f.name: type(f.default) for f in fields(EngineConfig)}
+    out = {}
+    for it in items:
+        k, _, v = it.partition("=")
+        if k not in types:
+            raise SystemExit(f"--set: unknown EngineConfig field {k!r}")
+        t = types[k]
+        out[k] = (v.lower() in ("1", "true", "yes")) if t is bool else t(v)
+    return out
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -51,6 +68,8 @@ def main():
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--quantization", default="", choices=["", "fp8"],
                     help="fp8 weight-only quantisation (BASELINE config 5); headline is bf16")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="EngineConfig override for A/B runs (e.g. fuse_attn_oproj=0)")
     ap.add_argument("--parallel", choices=["dp", "tp"], default="dp",
                     help="dp: one engine replica per GPU (default); tp: one engine over all GPUs")
     a = ap.parse_args()
@@ -79,7 +98,7 @@ def main():
                        max_num_batched_tokens=a.max_num_batched_tokens,
                        gpu_memory_utilization=a.gpu_memory_utilization,
                        use_graphs=not a.no_graphs, seed=1234, device=dev,
-                       quantization=a.quantization)
+                       quantization=a.quantization, **overrides(a.set))
     t0 = time.perf_counter()
     eng = LLMEngine(cfg)
     eng.runner.capture_all()
@@ -183,7 +202,8 @@ def main_tp(a):
                        max_num_batched_tokens=a.max_num_batched_tokens,
                        gpu_memory_utilization=a.gpu_memory_utilization,
                        use_graphs=not a.no_graphs, seed=1234, device="cuda",
-                       tensor_parallel_size=world, quantization=a.quantization)
+                       tensor_parallel_size=world, quantization=a.quantization,
+                       **overrides(a.set))
     port = int(os.environ.get("MASTER_PORT", "29511"))
     if rank > 0:
         from agentic_traffic_testing_amd.parallel.tp_engine import run_worker

@@ -142,6 +142,33 @@ def attn_sweep():
         print(row, flush=True)
 
 
+def grid_sweep():
+    """Does the launch grid (empty partition workgroups) cost decode attention time?"""
+    print("== decode attention v2 (us) vs grid z = max_parts (256-token partitions)")
+    hq, hkv, bs = 32, 8, 16
+    for B, ctx in ((1, 300), (5, 500), (5, 1000), (8, 1000), (5, 2000)):
+        nblk = math.ceil(ctx / bs)
+        nb = B * nblk + 8
+        k = torch.randn(nb, hkv, bs, 128, dtype=torch.bfloat16, device="cuda")
+        v = torch.randn(nb, hkv, 128, bs, dtype=torch.bfloat16, device="cuda")
+        bt = torch.randperm(nb, device="cuda")[:B * nblk].view(B, nblk).to(torch.int32)
+        kvlen = torch.full((B,), ctx, dtype=torch.int32, device="cuda")
+        qstart = torch.arange(B + 1, dtype=torch.int32, device="cuda")
+        q = torch.randn(B, hq, 128, dtype=torch.bfloat16, device="cuda")
+        out = torch.empty_like(q)
+        need = math.ceil(ctx / 256)
+        row = f"B={B:2d} ctx={ctx:5d} need={need:2d} |"
+        for mp in (need, 16, 64):
+            po = torch.empty(B * hkv * mp * 16 * 128, device="cuda")
+            pl = torch.empty(B * hkv * mp * 16, device="cuda")
+            cnt = torch.zeros(B * hkv, dtype=torch.int32, device="cuda")
+            t = timeit(lambda: ops.attention_decode_v2(q, k, v, bt, kvlen, qstart, 0.088, po, pl,
+                                                       cnt, mp, 256, out=out))
+            row += f" mp={mp:2d}: {t:6.1f}"
+        # padded batch: 8 extra dummy rows (kvlen 0) like a graph bucket
+        print(row, flush=True)
+
+
 if __name__ == "__main__":
     assert ops.native_available()
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
@@ -151,3 +178,5 @@ if __name__ == "__main__":
         attn_sweep()
     if what in ("all", "fp8"):
         fp8_sweep()
+    if what in ("all", "grid"):
+        grid_sweep()
