@@ -78,7 +78,6 @@ __global__ __launch_bounds__(WAVES * 64) void decode_attention_kernel(DecParams 
   __shared__ float lds_o[WAVES][G][kD + 4];
   __shared__ float lds_m[WAVES][G];
   __shared__ float lds_l[WAVES][G];
-  __shared__ float lds_w[64][G];
   __shared__ int lds_last;
 
   const int lane = threadIdx.x & 63;
@@ -88,17 +87,35 @@ __global__ __launch_bounds__(WAVES * 64) void decode_attention_kernel(DecParams 
   const int s = blockIdx.x;
   const int hk = blockIdx.y;
   const int part = blockIdx.z;
-  const int kvlen = p.seq_kvlen[s];
   const int PT = WAVES * 16 * TPW;
+  const int kv_begin = part * PT;
+  // ---- round trip 1: sequence length, query row and the block-table entries of this wave's
+  // tiles are independent loads - the entries are fetched unconditionally (index clamped to
+  // the table row) and only used for tiles inside the sequence
+  const int* bt = p.block_tables + static_cast<int64_t>(s) * p.bt_stride;
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);  // wave-uniform -> scalar loads
+  int kt[TPW], bte[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    kt[i] = kv_begin + (wid_u + i * WAVES) * 16;
+    bte[i] = bt[min(kt[i] >> p.bs_shift, p.bt_stride - 1)];
+  }
+  int kvlen = p.seq_kvlen[s];
+  int qrow = p.seq_qstart[s + 1] - 1;
+  // one wait for all of them (keeps the compiler from chaining the loads behind branches)
+  asm volatile("" : "+s"(kvlen), "+s"(qrow));
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) asm volatile("" : "+s"(bte[i]));
   const int nparts = (kvlen + PT - 1) / PT;
   if (part >= nparts) return;  // block-uniform (also kvlen == 0 dummy sequences)
-  const int kv_begin = part * PT;
   const int kv_end = min(kvlen, kv_begin + PT);
-  const int qrow = p.seq_qstart[s + 1] - 1;
   const int BS = 1 << p.bs_shift;
   const int64_t hs = static_cast<int64_t>(BS) * kD;
+  int page[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) page[i] = kt[i] < kv_end ? bte[i] : 0;
 
-  // ---- round trip 1: Q fragment + block-table entries of this wave's tiles -------------
+  // ---- round trip 2: Q fragment (needs the query row) + K/V fragments of all tiles --------
   frag8 qf[4];
   {
     const bool ok = col < G;
@@ -108,16 +125,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_attention_kernel(DecParams 
     for (int kk = 0; kk < 4; ++kk)
       qf[kk] = ok ? *reinterpret_cast<const frag8*>(qp + 8 * kk) : frag8{};
   }
-  const int* bt = p.block_tables + static_cast<int64_t>(s) * p.bt_stride;
-  int page[TPW];
-  int kt[TPW];
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    kt[i] = kv_begin + (wid + i * WAVES) * 16;
-    page[i] = kt[i] < kv_end ? bt[kt[i] >> p.bs_shift] : 0;
-  }
 
-  // ---- round trip 2: K/V fragments of all tiles -----------------------------------------
   TileFrags<T> f[TPW];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
@@ -245,31 +253,37 @@ __global__ __launch_bounds__(WAVES * 64) void decode_attention_kernel(DecParams 
   }
   __syncthreads();
   if (!lds_last) return;
-  // partition weights: lds_w[q][c] = 2^(lse_q - lse_max)
-  const int np = min(nparts, 64);
-  for (int e = threadIdx.x; e < np * G; e += WAVES * 64) {
-    const int q = e / G, cc = e % G;
-    lds_w[q][cc] = dev_load4(rpl, static_cast<uint32_t>(((sh * p.max_parts + q) * 16 + cc) * 4));
-  }
-  __syncthreads();
+  // merge: every merger thread streams (lse, partial) of 4 partitions per round trip and
+  // folds them into a running (max, weight sum, weighted sum) - one round trip for <= 4
+  // partitions (1k tokens at 256-token partitions)
   if (merger) {
-    float lmax = kNegInf;
-    for (int q = 0; q < np; ++q) lmax = fmaxf(lmax, lds_w[q][c]);
+    const int np = min(nparts, 64);
+    float m_run = kNegInf, wsum = 0.f;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float wsum = 0.f;
-    if (lmax != kNegInf) {
-      for (int q = 0; q < np; ++q) {
-        const float w = exp2f(lds_w[q][c] - lmax);  // lse == -inf -> weight 0
-        const int64_t base = (sh * p.max_parts + q) * 16 + c;
+    for (int q0 = 0; q0 < np; q0 += 4) {
+      float lse[4];
+      f32x4 pa[4], pb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t base = (sh * p.max_parts + min(q0 + u, np - 1)) * 16 + c;
         const uint32_t off = static_cast<uint32_t>((base * kD + d0) * 4);
-        const f32x4 a = __builtin_bit_cast(f32x4, dev_load16(rpo, off));
-        const f32x4 b = __builtin_bit_cast(f32x4, dev_load16(rpo, off + 16));
-        wsum += w;
+        lse[u] = dev_load4(rpl, static_cast<uint32_t>(base * 4));
+        pa[u] = __builtin_bit_cast(f32x4, dev_load16(rpo, off));
+        pb[u] = __builtin_bit_cast(f32x4, dev_load16(rpo, off + 16));
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (q0 + u >= np || lse[u] == kNegInf) continue;  // lse == -inf -> weight 0
+        const float m_new = fmaxf(m_run, lse[u]);
+        const float sc = exp2f(m_run - m_new);  // m_run == -inf -> 0
+        const float w = exp2f(lse[u] - m_new);
+        wsum = wsum * sc + w;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          acc[j] += w * a[j];
-          acc[4 + j] += w * b[j];
+          acc[j] = acc[j] * sc + w * pa[u][j];
+          acc[4 + j] = acc[4 + j] * sc + w * pb[u][j];
         }
+        m_run = m_new;
       }
     }
     const float inv = wsum > 0.f ? 1.f / wsum : 0.f;
