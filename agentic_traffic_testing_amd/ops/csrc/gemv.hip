@@ -373,38 +373,52 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
   }
 }
 
-// Weight-stream cache policy.  Measured on the fan-out bench (profiles/bench_r1_ab_nt.log):
-// register-destination nt loads made every decode GEMV slower (gate_up 42 -> 48 us, down
-// 23 -> 29 us), so the default policy stays; ATTA_NT_WEIGHTS=1 re-enables nt for A/B runs.
-static bool nt_weights() {
-  static const bool on = [] {
+// Weight-stream cache policy.  Non-temporal (nt) weight loads: every decode weight byte is
+// read once per step by one CU, so keeping it out of the caches helps - but only with the
+// pre-shuffled layout (one contiguous 1 KiB per wave instruction): there nt lifted the
+// fan-out bench from 703 to 756 tok/s (profiles/bench_r1_v10_nt.log).  On the row-major
+// layout (16 rows x 64 B per instruction) nt made every GEMV slower (gate_up 42 -> 48 us,
+// profiles/bench_r1_ab_nt.log), so it stays off there.  ATTA_NT_WEIGHTS=0 disables it for
+// A/B runs, =1 forces it on for row-major weights too.
+static int nt_weights() {
+  static const int mode = [] {
     const char* e = std::getenv("ATTA_NT_WEIGHTS");
-    return e != nullptr && e[0] == '1';
+    return e == nullptr ? -1 : (e[0] == '1' ? 1 : 0);  // -1 = default policy per layout
   }();
-  return on;
+  return mode;
 }
 
 template <int WAVES, int UNROLL, int MT, int EPI>
 static void launch_t(int dtype, dim3 grid, hipStream_t st, const SkinnyParams& p) {
-  const bool nt = nt_weights();
+  const int mode = nt_weights();
+  const bool shuffled = p.ps || p.wscale != nullptr;
+  const bool nt = shuffled ? mode != 0 : mode == 1;
   const dim3 blk(WAVES * 64);
+#define ATTA_SK(T_, U_, NT_, PS_, W8_) \
+  skinny_kernel<T_, WAVES, U_, MT, EPI, NT_, PS_, W8_><<<grid, blk, 0, st>>>(p)
   if (p.wscale != nullptr) {
     // fp8 weights (pre-shuffled by construction): a 16-byte lane load carries two K steps,
     // so the stage is twice as deep to keep the same bytes in flight per wave
     constexpr int U8 = UNROLL * 2;
-    if (dtype == 0) skinny_kernel<__bf16, WAVES, U8, MT, EPI, false, true, true><<<grid, blk, 0, st>>>(p);
-    else skinny_kernel<_Float16, WAVES, U8, MT, EPI, false, true, true><<<grid, blk, 0, st>>>(p);
+    if (dtype == 0) {
+      if (nt) ATTA_SK(__bf16, U8, true, true, true); else ATTA_SK(__bf16, U8, false, true, true);
+    } else {
+      if (nt) ATTA_SK(_Float16, U8, true, true, true); else ATTA_SK(_Float16, U8, false, true, true);
+    }
     return;
   }
   if (dtype == 0) {
-    if (p.ps) skinny_kernel<__bf16, WAVES, UNROLL, MT, EPI, false, true><<<grid, blk, 0, st>>>(p);
-    else if (nt) skinny_kernel<__bf16, WAVES, UNROLL, MT, EPI, true><<<grid, blk, 0, st>>>(p);
-    else skinny_kernel<__bf16, WAVES, UNROLL, MT, EPI, false><<<grid, blk, 0, st>>>(p);
+    if (p.ps && nt) ATTA_SK(__bf16, UNROLL, true, true, false);
+    else if (p.ps) ATTA_SK(__bf16, UNROLL, false, true, false);
+    else if (nt) ATTA_SK(__bf16, UNROLL, true, false, false);
+    else ATTA_SK(__bf16, UNROLL, false, false, false);
   } else {
-    if (p.ps) skinny_kernel<_Float16, WAVES, UNROLL, MT, EPI, false, true><<<grid, blk, 0, st>>>(p);
-    else if (nt) skinny_kernel<_Float16, WAVES, UNROLL, MT, EPI, true><<<grid, blk, 0, st>>>(p);
-    else skinny_kernel<_Float16, WAVES, UNROLL, MT, EPI, false><<<grid, blk, 0, st>>>(p);
+    if (p.ps && nt) ATTA_SK(_Float16, UNROLL, true, true, false);
+    else if (p.ps) ATTA_SK(_Float16, UNROLL, false, true, false);
+    else if (nt) ATTA_SK(_Float16, UNROLL, true, false, false);
+    else ATTA_SK(_Float16, UNROLL, false, false, false);
   }
+#undef ATTA_SK
 }
 
 template <int EPI>

@@ -29,3 +29,24 @@ rows.sort()
 if rows:
     span = (rows[-1][1] - rows[0][0]) / 1e6
     print(f"\nwall span of traced kernels: {span:.1f} ms; busy {all_t/1e3:.1f} ms ({100*all_t/1e3/span:.1f}%)")
+
+# Gaps between back-to-back kernels of the decode step (graph replay): for every pair of
+# consecutive dispatches where both are atta decode kernels, start[i+1] - end[i].
+def short_name(n):
+    for key in ("skinny_kernel", "decode_attention_kernel", "sample_finalize", "oneshot"):
+        if key in n:
+            return key
+    return None
+
+
+gaps = defaultdict(list)
+for (s0, e0, n0), (s1, e1, n1) in zip(rows, rows[1:]):
+    a, b = short_name(n0), short_name(n1)
+    if a and b and 0 <= s1 - e0 < 100_000:  # same step (< 100 us apart)
+        gaps[f"{a} -> {b}"].append((s1 - e0) / 1e3)
+if gaps:
+    import statistics
+    print("\ninter-kernel gaps inside decode steps (us): pair, count, median, p90")
+    for k, v in sorted(gaps.items(), key=lambda kv: -len(kv[1])):
+        v.sort()
+        print(f"  {k:50s} {len(v):7d} {statistics.median(v):7.2f} {v[int(0.9 * (len(v) - 1))]:7.2f}")
