@@ -308,15 +308,6 @@ void attention_decode_v2(at::Tensor out, at::Tensor part_out, at::Tensor part_ls
            "attention_decode_v2");
 }
 
-void prefetch(const at::Tensor& t, int64_t blocks, int64_t inflight) {
-  check_dev(t, "prefetch");
-  TORCH_CHECK(t.is_contiguous(), "prefetch: contiguous tensor");
-  const at::DeviceGuard g(t.device());
-  check_rc(atta_prefetch(t.data_ptr(), t.numel() * t.element_size(), static_cast<int>(blocks),
-                         static_cast<int>(inflight), cur_stream()),
-           "prefetch");
-}
-
 void skinny_variant(at::Tensor y, const at::Tensor& x, const at::Tensor& w, int64_t variant) {
   check_skinny(x, w, "skinny_variant");
   TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.scalar_type() == at::kBFloat16,
@@ -411,7 +402,6 @@ TORCH_LIBRARY(atta, m) {
       "Tensor temperature, Tensor seeds, Tensor steps, int finalize, int vocab_offset, "
       "int waves, bool preshuffled=False, Tensor? w_scale=None) -> ()");
   m.def("sample_finalize(Tensor(a!) tokens, Tensor keys, int n_tiles) -> ()");
-  m.def("prefetch(Tensor t, int blocks, int inflight) -> ()");
   m.def("skinny_gemm(Tensor(a!) y, Tensor x, Tensor w, Tensor? residual, int waves, "
         "bool preshuffled=False, Tensor? w_scale=None) -> ()");
   m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
@@ -447,7 +437,6 @@ TORCH_LIBRARY_IMPL(atta, CUDA, m) {
   m.impl("fused_gate_up_silu", &fused_gate_up_silu);
   m.impl("fused_lm_head_sample", &fused_lm_head_sample);
   m.impl("sample_finalize", &sample_finalize);
-  m.impl("prefetch", &prefetch);
   m.impl("attention_decode_v2", &attention_decode_v2);
   m.impl("skinny_variant", &skinny_variant);
 }

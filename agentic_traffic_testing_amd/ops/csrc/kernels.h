@@ -70,9 +70,6 @@ int atta_attention_decode_v2(void* out, float* part_out, float* part_lse, int* c
                              int64_t q_stride, int64_t out_stride, float scale, int dtype,
                              hipStream_t stream);
 
-// Stream [ptr, ptr + bytes) through the cache hierarchy (Infinity-Cache warm-up).
-int atta_prefetch(const void* ptr, int64_t bytes, int blocks, int inflight, hipStream_t stream);
-
 int atta_skinny_variant(void* y, const void* x, const void* w, int M, int N, int K,
                         int variant, hipStream_t stream);
 

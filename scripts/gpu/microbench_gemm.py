@@ -169,87 +169,6 @@ def grid_sweep():
         print(row, flush=True)
 
 
-def mall_sweep():
-    """Does warming the Infinity Cache help the next GEMV, and what does a concurrent
-    prefetch cost decode attention?"""
-    nat = ops._native()
-    H = 4096
-    print("== o_proj / qkv / down GEMV (us): cold vs after a MALL prefetch of its weights")
-    for name, N, K, waves in (("o", 4096, 4096, 8), ("qkv", 6144, 4096, 4), ("down", 4096, 14336, 8)):
-        ncopy = max(3, math.ceil(900e6 / (N * K * 2)))
-        ws = [ops.preshuffle(torch.randn(N, K, dtype=torch.bfloat16, device="cuda") * 0.02)
-              for _ in range(ncopy)]
-        x = torch.randn(5, K, dtype=torch.bfloat16, device="cuda")
-        row = f"{name:5s} {N}x{K}:"
-        for mode in ("cold", "pf64x4", "pf256x4", "warm"):
-            ts = []
-            for it in range(3 * ncopy):
-                w = ws[it % ncopy]
-                if mode.startswith("pf"):
-                    b, f = mode[2:].split("x")
-                    nat.prefetch(w, int(b), int(f))
-                elif mode == "warm":
-                    ops.linear(x, w, waves=waves, preshuffled=True)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                ops.linear(x, w, waves=waves, preshuffled=True)
-                e1.record()
-                torch.cuda.synchronize()
-                if it >= ncopy:
-                    ts.append(e0.elapsed_time(e1) * 1000)
-            row += f" {mode} {statistics.median(ts):6.1f}"
-        print(row, flush=True)
-        del ws
-    print("== decode attention (B=5, ctx=1000) with a concurrent prefetch of 33.5 MB on a side "
-          "stream (us, attention events only); prefetch alone in parentheses")
-    hq, hkv, bs, B, ctx = 32, 8, 16, 5, 1000
-    nblk = math.ceil(ctx / bs)
-    nb = B * nblk + 8
-    sets = [(torch.randn(nb, hkv, bs, 128, dtype=torch.bfloat16, device="cuda"),
-             torch.randn(nb, hkv, 128, bs, dtype=torch.bfloat16, device="cuda"),
-             torch.empty(H * H, dtype=torch.bfloat16, device="cuda")) for _ in range(12)]
-    bt = torch.randperm(nb, device="cuda")[:B * nblk].view(B, nblk).to(torch.int32)
-    kvlen = torch.full((B,), ctx, dtype=torch.int32, device="cuda")
-    qstart = torch.arange(B + 1, dtype=torch.int32, device="cuda")
-    q = torch.randn(B, hq, 128, dtype=torch.bfloat16, device="cuda")
-    out = torch.empty_like(q)
-    mp = 16
-    po = torch.empty(B * hkv * mp * 16 * 128, device="cuda")
-    pl = torch.empty(B * hkv * mp * 16, device="cuda")
-    cnt = torch.zeros(B * hkv, dtype=torch.int32, device="cuda")
-    side = torch.cuda.Stream()
-    main = torch.cuda.current_stream()
-    row = ""
-    for cfg in ("none", "16x2", "32x2", "64x2", "64x4", "128x4", "256x4"):
-        ts, tp = [], []
-        for it in range(36):
-            k, v, w = sets[it % 12]
-            ev = torch.cuda.Event()
-            ev.record(main)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            if cfg != "none":
-                b, f = cfg.split("x")
-                with torch.cuda.stream(side):
-                    side.wait_event(ev)
-                    p0.record(side)
-                    nat.prefetch(w, int(b), int(f))
-                    p1.record(side)
-            e0.record(main)
-            ops.attention_decode_v2(q, k, v, bt, kvlen, qstart, 0.088, po, pl, cnt, mp, 256,
-                                    out=out)
-            e1.record(main)
-            torch.cuda.synchronize()
-            if it >= 12:
-                ts.append(e0.elapsed_time(e1) * 1000)
-                if cfg != "none":
-                    tp.append(p0.elapsed_time(p1) * 1000)
-        row += f" {cfg}: {statistics.median(ts):5.1f}"
-        if tp:
-            row += f" ({statistics.median(tp):5.1f})"
-    print(row, flush=True)
-
-
 if __name__ == "__main__":
     assert ops.native_available()
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
@@ -259,7 +178,5 @@ if __name__ == "__main__":
         attn_sweep()
     if what in ("all", "fp8"):
         fp8_sweep()
-    if what == "mall":
-        mall_sweep()
     if what in ("all", "grid"):
         grid_sweep()
