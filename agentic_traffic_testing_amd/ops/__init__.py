@@ -171,6 +171,11 @@ DECODE_WAVES = {
     "down": {"rm": 16, "ps": 8, "fp8": 16},
     "lm_head": {"rm": 16, "ps": 16, "fp8": 16},
 }
+# tuning override: ATTA_DECODE_WAVES="qkv.ps=8,down.fp8=16"
+for _item in filter(None, os.environ.get("ATTA_DECODE_WAVES", "").split(",")):
+    _key, _, _val = _item.partition("=")
+    _proj, _, _fmt = _key.strip().partition(".")
+    DECODE_WAVES[_proj][_fmt] = int(_val)
 
 
 def decode_waves(proj: str, preshuffled: bool = False, fp8: bool = False) -> int:
