@@ -84,7 +84,8 @@ def _common_llm_env() -> list:
             ("LLM_MAX_MODEL_LEN", "4096"), ("LLM_PROMPT_SAFETY_MARGIN_TOKENS", "128"),
             ("LLM_METRICS_ENABLED", "1"), ("LLM_METRICS_INCLUDE_TOKENS", "1"),
             ("LLM_METRICS_PREFIX", "llm"), ("LLM_TENSOR_PARALLEL_SIZE", "1"),
-            ("LLM_LOAD_FORMAT", "auto"),
+            ("LLM_LOAD_FORMAT", "auto"), ("LLM_DATA_PARALLEL_SIZE", "1"),
+            ("LLM_QUANTIZATION", ""),
             ("LLM_MODEL", "meta-llama/Llama-3.1-8B-Instruct")]
     return [f"{k}=${{{k}:-{v}}}" for k, v in keys]
 
@@ -109,7 +110,8 @@ def llm_service(distributed: bool) -> dict:
                     "--max-num-seqs", "${LLM_MAX_NUM_SEQS:-12}",
                     "--max-num-batched-tokens", "${LLM_MAX_NUM_BATCHED_TOKENS:-8192}",
                     "--gpu-memory-utilization", "${LLM_GPU_MEMORY_UTILIZATION:-0.90}",
-                    "--tensor-parallel-size", "${LLM_TENSOR_PARALLEL_SIZE:-1}"],
+                    "--tensor-parallel-size", "${LLM_TENSOR_PARALLEL_SIZE:-1}",
+                    "--data-parallel-size", "${LLM_DATA_PARALLEL_SIZE:-1}"],
         "volumes": ["hf_model_cache:/root/.cache/huggingface"],
         "ports": ["8000:8000"],
         # ROCm device access (replaces the NVIDIA runtime reservation)

@@ -397,7 +397,8 @@ def make_parser() -> argparse.ArgumentParser:
     p.add_argument("--max-num-batched-tokens", type=int, default=None)
     p.add_argument("--gpu-memory-utilization", type=float, default=None)
     p.add_argument("--tensor-parallel-size", "--tp-size", type=int, default=None)
-    p.add_argument("--quantization", "-q", default=None, choices=["fp8"],
+    p.add_argument("--quantization", "-q", choices=["fp8"],
+                   default=os.environ.get("LLM_QUANTIZATION", "").lower() or None,
                    help="fp8 weight-only quantisation (OCP e4m3fn, per-row scales)")
     p.add_argument("--data-parallel-size", "--dp-size", type=int, default=1,
                    help="engine replicas, one per GPU, behind a router on --port "
