@@ -112,6 +112,10 @@ class AsyncEngine:
         except RuntimeError:  # loop closed
             pass
 
+    def _fail_pending(self, err: BaseException):
+        while self._pending:
+            self._deliver(self._pending.popleft()[0], err)
+
     def _run(self):
         eng = self.engine
         while not self._stop.is_set():
@@ -145,6 +149,11 @@ class AsyncEngine:
                 for s in list(eng.scheduler.running) + list(eng.scheduler.waiting):
                     eng.abort(s.request_id)
                     self._deliver(s.request_id, err)
+                dead = eng.dead_ranks() if hasattr(eng, "dead_ranks") else []
+                if dead:  # a TP peer is gone: no later step can succeed -> /health 503
+                    self.last_error = f"TP ranks {dead} died\n" + self.last_error
+                    self._fail_pending(RuntimeError(f"engine dead: TP ranks {dead} died"))
+                    return
                 continue
             for o in outs:
                 self._deliver(o.request_id, o)

@@ -336,12 +336,22 @@ class ModelRunner:
 
     # -- TP worker side ------------------------------------------------------------------
     def serve_worker(self, channel, reader: int) -> None:
-        """TP rank > 0: replay rank 0's steps until it publishes OP_STOP / closes."""
+        """TP rank > 0: replay rank 0's steps until it publishes OP_STOP / closes.
+
+        Liveness: the worker registers its pid on the channel (rank 0 fails its next publish
+        naming a dead worker) and waits in 1 s slices, raising when rank 0's process is gone
+        so an orphaned worker exits instead of holding its GPU forever."""
         last = 0
+        if hasattr(channel, "register_reader"):
+            channel.register_reader(reader)
         while True:
-            msg = channel.receive(reader, last, -1.0)
+            msg = channel.receive(reader, last, 1.0)
             if msg is None:
-                return
+                if channel.closed:
+                    return
+                if not getattr(channel, "writer_alive", True):
+                    raise RuntimeError(f"TP rank {reader + 1}: rank 0 died; worker exiting")
+                continue
             last, data = msg
             hdr = data[:HDR_WORDS]
             op = int(hdr[0])

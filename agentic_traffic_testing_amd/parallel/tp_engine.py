@@ -141,6 +141,15 @@ class TPEngine(LLMEngine):
         runner.capture_all()
         self._closed = False
 
+    def dead_ranks(self) -> list[int]:
+        """TP ranks whose process is gone (spawned children, or torchrun peers that had
+        registered on the step channel) - SURVEY §5.3 TP-rank liveness."""
+        dead = {i + 1 for i, p in enumerate(self.procs) if not p.is_alive()}
+        ch = getattr(self, "channel", None)
+        if ch is not None:
+            dead.update(r + 1 for r in ch.dead_readers())
+        return sorted(dead)
+
     def shutdown(self):
         if getattr(self, "_closed", True):
             return

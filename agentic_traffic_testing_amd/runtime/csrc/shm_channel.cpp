@@ -13,7 +13,15 @@
 // after every reader has acknowledged message seq-1 (so the slot it overwrites - seq-2's -
 // is dead), then stores `seq` with release ordering.  Readers spin briefly, then back off
 // with short sleeps, copy the slot out and store their ack (release).
+//
+// Rank liveness (SURVEY §5.3 "TP-rank liveness"): the header records the writer's pid and
+// every attached reader's pid.  A writer waiting for acks checks its readers' pids while it
+// backs off and fails the publish naming the dead rank; a reader can ask whether the writer
+// is still alive between timed receives, so a TP worker exits when rank 0 dies instead of
+// spinning forever.
+#include <errno.h>
 #include <fcntl.h>
+#include <signal.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <time.h>
@@ -34,17 +42,24 @@ namespace py = pybind11;
 namespace {
 
 constexpr int kMaxReaders = 64;
-constexpr uint64_t kMagic = 0x4154544153484d31ull;  // "ATTASHM1"
+constexpr uint64_t kMagic = 0x4154544153484d32ull;  // "ATTASHM2"
 
 struct alignas(64) Header {
   uint64_t magic;
   uint32_t capacity;   // int32 words per slot
   uint32_t n_readers;
+  int32_t writer_pid;
   alignas(64) std::atomic<uint64_t> seq;
   alignas(64) std::atomic<uint32_t> closed;
   alignas(64) std::atomic<uint64_t> acks[kMaxReaders];
+  std::atomic<int32_t> reader_pids[kMaxReaders];  // 0 = not attached yet
   uint32_t slot_words[2];
 };
+
+// true unless `pid` provably no longer exists (EPERM: alive but not ours)
+inline bool pid_alive(int32_t pid) {
+  return pid <= 0 || kill(static_cast<pid_t>(pid), 0) == 0 || errno != ESRCH;
+}
 
 inline void cpu_relax() { __builtin_ia32_pause(); }
 
@@ -93,6 +108,8 @@ class ShmChannel {
     if (create) {
       hdr_->capacity = static_cast<uint32_t>(capacity_words);
       hdr_->n_readers = static_cast<uint32_t>(n_readers);
+      hdr_->writer_pid = static_cast<int32_t>(getpid());
+      for (auto& r : hdr_->reader_pids) r.store(0, std::memory_order_relaxed);
       hdr_->seq.store(0, std::memory_order_relaxed);
       hdr_->closed.store(0, std::memory_order_relaxed);
       for (auto& a : hdr_->acks) a.store(0, std::memory_order_relaxed);
@@ -113,6 +130,21 @@ class ShmChannel {
   int n_readers() const { return static_cast<int>(hdr_->n_readers); }
   uint64_t seq() const { return hdr_->seq.load(std::memory_order_acquire); }
   bool closed() const { return hdr_->closed.load(std::memory_order_acquire) != 0; }
+  bool writer_alive() const { return pid_alive(hdr_->writer_pid); }
+
+  // A reader announces its pid so the writer can tell a dead rank from a slow one.
+  void register_reader(int reader) {
+    check_reader(reader);
+    hdr_->reader_pids[reader].store(static_cast<int32_t>(getpid()), std::memory_order_release);
+  }
+
+  // Reader ids whose registered process no longer exists.
+  py::list dead_readers() const {
+    py::list out;
+    for (uint32_t r = 0; r < hdr_->n_readers; ++r)
+      if (!pid_alive(hdr_->reader_pids[r].load(std::memory_order_acquire))) out.append(r);
+    return out;
+  }
 
   // Publish one message; blocks (GIL released) until the slot is free.  Returns its seq.
   uint64_t publish(py::array_t<int32_t, py::array::c_style | py::array::forcecast> a,
@@ -121,26 +153,28 @@ class ShmChannel {
     if (n > static_cast<int64_t>(hdr_->capacity)) throw std::length_error("message too large");
     const int32_t* src = a.data();
     const uint64_t next = hdr_->seq.load(std::memory_order_relaxed) + 1;
-    bool ok = true;
+    int rc = 0;
     {
       py::gil_scoped_release nogil;
-      ok = wait_acks(next - 1, timeout_s);
-      if (ok) {
+      rc = wait_acks(next - 1, timeout_s);
+      if (rc == 0) {
         int32_t* dst = slots_ + static_cast<size_t>(next & 1) * hdr_->capacity;
         std::memcpy(dst, src, static_cast<size_t>(n) * 4);
         hdr_->slot_words[next & 1] = static_cast<uint32_t>(n);
         hdr_->seq.store(next, std::memory_order_release);
       }
     }
-    if (!ok) throw std::runtime_error("shm channel: readers did not acknowledge in time");
+    if (rc > 0)
+      throw std::runtime_error("shm channel: reader " + std::to_string(rc - 1) +
+                               " (TP rank " + std::to_string(rc) + ") died");
+    if (rc < 0) throw std::runtime_error("shm channel: readers did not acknowledge in time");
     return next;
   }
 
   // Wait for a message newer than `last_seq`; returns (seq, int32 array) or None when the
   // channel was closed or the timeout (<0: forever) expired.
   py::object receive(int reader, uint64_t last_seq, double timeout_s) {
-    if (reader < 0 || reader >= static_cast<int>(hdr_->n_readers))
-      throw std::out_of_range("reader id");
+    check_reader(reader);
     uint64_t s = 0;
     bool got = false;
     py::array_t<int32_t> out;
@@ -177,20 +211,30 @@ class ShmChannel {
   void close_channel() { hdr_->closed.store(1, std::memory_order_release); }
 
  private:
-  bool wait_acks(uint64_t target, double timeout_s) {
+  void check_reader(int reader) const {
+    if (reader < 0 || reader >= static_cast<int>(hdr_->n_readers))
+      throw std::out_of_range("reader id");
+  }
+
+  // 0: every reader acknowledged `target`; -1: timeout; r + 1: reader r's process is gone.
+  int wait_acks(uint64_t target, double timeout_s) {
     const auto t0 = std::chrono::steady_clock::now();
     uint64_t spins = 0;
     for (uint32_t r = 0; r < hdr_->n_readers; ++r) {
       while (hdr_->acks[r].load(std::memory_order_acquire) < target) {
-        if (timeout_s >= 0 && (spins & 1023) == 0) {
-          const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0)
-                                .count();
-          if (el > timeout_s) return false;
+        if ((spins & 1023) == 1023) {
+          if (!pid_alive(hdr_->reader_pids[r].load(std::memory_order_acquire)))
+            return static_cast<int>(r) + 1;
+          if (timeout_s >= 0) {
+            const double el =
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (el > timeout_s) return -1;
+          }
         }
         backoff(spins);
       }
     }
-    return true;
+    return 0;
   }
 
   std::string name_;
@@ -210,6 +254,9 @@ void register_shm_channel(py::module_& m) {
       .def_property_readonly("n_readers", &ShmChannel::n_readers)
       .def_property_readonly("seq", &ShmChannel::seq)
       .def_property_readonly("closed", &ShmChannel::closed)
+      .def_property_readonly("writer_alive", &ShmChannel::writer_alive)
+      .def("register_reader", &ShmChannel::register_reader, py::arg("reader"))
+      .def("dead_readers", &ShmChannel::dead_readers)
       .def("publish", &ShmChannel::publish, py::arg("data"), py::arg("timeout_s") = -1.0)
       .def("receive", &ShmChannel::receive, py::arg("reader"), py::arg("last_seq"),
            py::arg("timeout_s") = -1.0)

@@ -26,6 +26,7 @@ import argparse
 import asyncio
 import json
 import os
+import random
 import sys
 import time
 import uuid
@@ -56,6 +57,11 @@ class Settings:
         self.apply_template = _env_bool("LLM_APPLY_CHAT_TEMPLATE", "1")
         self.temperature = float(e.get("LLM_TEMPERATURE", "0.2"))
         self.watchdog_s = float(e.get("LLM_WATCHDOG_SECONDS", "120"))
+        # fault injection: exercise the agents' error / timeout paths
+        self.fault_fail_rate = float(e.get("LLM_FAULT_FAIL_RATE") or "0")
+        self.fault_delay_s = float(e.get("LLM_FAULT_DELAY_MS") or "0") / 1000.0
+        self.fault_step_delay_s = float(e.get("LLM_FAULT_STEP_DELAY_MS") or "0") / 1000.0
+        self.fault_rng = random.Random(int(e.get("LLM_FAULT_SEED") or "0"))
 
 
 class ServerState:
@@ -222,6 +228,11 @@ async def handle_chat(request: web.Request) -> web.Response:
         queue_wait = 0.0
         final = None
         try:
+            if st.s.fault_delay_s > 0:
+                await asyncio.sleep(st.s.fault_delay_s)
+            if st.s.fault_fail_rate > 0 and st.s.fault_rng.random() < st.s.fault_fail_rate:
+                span.set_attribute("app.fault_injected", True)
+                raise RuntimeError("injected fault (LLM_FAULT_FAIL_RATE)")
             wait_span = st.tracer.start_span("llm.time_to_first_token")
             gen_span = None
             t_sub = time.monotonic()
@@ -356,7 +367,9 @@ async def run_server(args) -> None:
     t0 = time.time()
     eng = build_engine(args)
     state = ServerState(eng, None, model_name=args.model)
-    aeng = AsyncEngine(eng, on_step=state.on_step).start()
+    aeng = AsyncEngine(eng, on_step=state.on_step)
+    aeng.fault_injection_delay_s = state.s.fault_step_delay_s
+    aeng.start()
     state.aengine = aeng
     state.export_config()
     app = create_app(state)

@@ -35,6 +35,49 @@ def test_shm_channel_roundtrip():
     assert r.receive(0, 2, -1) is None  # closed channel wakes blocked readers
 
 
+def _register_and_exit(name, reader):
+    ShmChannel(name).register_reader(reader)
+
+
+def _create_and_exit(name, q):
+    ch = ShmChannel(name, 16, 1, create=True)  # noqa: F841  (the segment outlives no one)
+    q.put("created")
+    import time
+
+    time.sleep(0.5)
+    os._exit(0)  # skip the destructor's shm_unlink: the segment stays, its writer is gone
+
+
+def test_shm_channel_rank_liveness():
+    """SURVEY §5.3 TP-rank liveness: rank 0 names a dead worker instead of waiting forever,
+    and a worker can tell that rank 0 is gone."""
+    name = f"atta_pytest_live_{os.getpid()}"
+    w = ShmChannel(name, 16, 2, create=True)
+    assert w.writer_alive and w.dead_readers() == []
+    w.register_reader(0)  # reader 0 = this (live) process
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_register_and_exit, args=(name, 1))
+    p.start()
+    p.join(60)
+    assert w.dead_readers() == [1]
+    w.publish(np.zeros(1, dtype=np.int32))  # seq 1: nobody has to have acked seq 0
+    ShmChannel(name).receive(0, 0, 1.0)
+    with pytest.raises(RuntimeError, match="died"):
+        w.publish(np.zeros(1, dtype=np.int32), 30.0)  # reader 1 never acks, and is dead
+    del w
+
+    name2 = name + "_w"
+    q = ctx.Queue()
+    p = ctx.Process(target=_create_and_exit, args=(name2, q))
+    p.start()
+    assert q.get(timeout=60) == "created"
+    r = ShmChannel(name2)
+    p.join(60)
+    assert not r.writer_alive
+    assert r.receive(0, 0, 0.05) is None
+    os.remove(f"/dev/shm/{name2}")
+
+
 def _comm_worker(rank, world, port, q):
     try:
         from agentic_traffic_testing_amd.parallel.comm import init_distributed
