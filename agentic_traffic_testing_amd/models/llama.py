@@ -290,11 +290,12 @@ class LlamaModel:
         return x
 
     def forward(self, input_ids: torch.Tensor, md: AttnMeta, k_caches, v_caches,
-                part_out=None, part_lse=None, num_parts: int = 1, part_tokens: int = 256):
+                part_out=None, part_lse=None, num_parts: int = 1, part_tokens: int = 256,
+                prev_tokens=None, feed_prev=None):
         """Returns the final normed hidden state rows [T, H]."""
         cfg = self.cfg
         eps = cfg.rms_norm_eps
-        h = F.embedding(input_ids, self.embed)
+        h = ops.embed(self.embed, input_ids, prev_tokens, feed_prev)
         T = h.shape[0]
         residual = torch.empty_like(h)
         nq, nkv, D = self.n_heads, self.n_kv_heads, self.head_dim
@@ -331,7 +332,8 @@ class LlamaModel:
                 and (self.n_heads * self.head_dim) % step == 0)
 
     def forward_decode(self, input_ids: torch.Tensor, md: AttnMeta, k_caches, v_caches, ws: dict,
-                       temperature, seeds, steps) -> torch.Tensor:
+                       temperature, seeds, steps, prev_tokens=None,
+                       feed_prev=None) -> torch.Tensor:
         """Fused decode step (every sequence has one query token); returns sampled ids.
 
         Per layer: [RMSNorm+QKV+RoPE+KV-write] -> [paged attention, in-kernel split-K
@@ -341,7 +343,7 @@ class LlamaModel:
         eps = self.cfg.rms_norm_eps
         nq, nkv = self.n_heads, self.n_kv_heads
         B = input_ids.shape[0]
-        residual = F.embedding(input_ids, self.embed)
+        residual = ops.embed(self.embed, input_ids, prev_tokens, feed_prev)
         q = ws["q"][:B]
         attn = ws["attn"][:B]
         act = ws["act"][:B]

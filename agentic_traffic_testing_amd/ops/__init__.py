@@ -95,6 +95,31 @@ def silu_and_mul(x: torch.Tensor, out: torch.Tensor | None = None):
     return out
 
 
+def embed(table: torch.Tensor, ids: torch.Tensor, prev: torch.Tensor | None = None,
+          feed_prev: torch.Tensor | None = None, out: torch.Tensor | None = None):
+    """Token-embedding gather.  With the int32 device flag ``feed_prev[0]`` set, row r takes
+    token ``prev[r]`` (the previous step's device samples) instead of ``ids[r]`` - how an
+    async-decode look-ahead step gets inputs the host has not seen yet."""
+    T = ids.shape[0]
+    if not table.is_cuda:
+        src = ids
+        if prev is not None and feed_prev is not None and int(feed_prev[0]) != 0:
+            src = prev[:T]
+        r = torch.nn.functional.embedding(src.long().clamp(0, table.shape[0] - 1), table)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    if out is None:
+        out = torch.empty(T, table.shape[1], dtype=table.dtype, device=table.device)
+    if ids.dtype != torch.int32:
+        ids = ids.to(torch.int32)
+    if prev is None or feed_prev is None:
+        prev = feed_prev = None
+    _native().embed(out, table, ids.contiguous(), prev, feed_prev)
+    return out
+
+
 def rope_cache(qkv, positions, slot_mapping, cos_sin, k_cache, v_cache, n_q_heads, n_kv_heads,
                head_dim, q_out: torch.Tensor | None = None):
     """Rotate q/k, write k/v to the paged cache; returns q [T, Hq, D]."""

@@ -63,6 +63,33 @@ void silu_and_mul(at::Tensor out, const at::Tensor& x) {
            "silu_and_mul");
 }
 
+// prev (int64) is read only while *feed_prev != 0, i.e. for async-decode look-ahead steps
+// (decode batches, rows <= the sampler output buffer); prefill steps leave the flag 0.
+void embed(at::Tensor out, const at::Tensor& table, const at::Tensor& ids,
+           const c10::optional<at::Tensor>& prev, const c10::optional<at::Tensor>& feed_prev) {
+  check_dev(table, "table");
+  TORCH_CHECK(table.dim() == 2 && table.is_contiguous(), "embed: table [V, H] contiguous");
+  TORCH_CHECK(out.dim() == 2 && out.size(1) == table.size(1) && out.stride(1) == 1,
+              "embed: out [T, H]");
+  TORCH_CHECK(ids.scalar_type() == at::kInt && ids.is_contiguous() && ids.numel() >= out.size(0),
+              "embed: ids int32 [T]");
+  TORCH_CHECK(out.scalar_type() == table.scalar_type(), "embed: dtype");
+  const int64_t* pv = nullptr;
+  const int* fp = nullptr;
+  if (feed_prev.has_value()) {
+    TORCH_CHECK(prev.has_value() && prev->scalar_type() == at::kLong && prev->is_contiguous(),
+                "embed: prev int64");
+    TORCH_CHECK(feed_prev->scalar_type() == at::kInt && feed_prev->numel() >= 1, "embed: flag");
+    pv = prev->data_ptr<int64_t>();
+    fp = feed_prev->data_ptr<int>();
+  }
+  dtype_code(table);
+  const at::DeviceGuard g(table.device());
+  check_rc(atta_embed(out.data_ptr(), table.data_ptr(), ids.data_ptr<int>(), pv, fp, out.size(0),
+                      table.size(1), table.size(0), out.stride(0), cur_stream()),
+           "embed");
+}
+
 void rope_cache(at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache, const at::Tensor& qkv,
                 const at::Tensor& positions, const at::Tensor& slot_mapping,
                 const at::Tensor& cos_sin, int64_t n_q_heads, int64_t n_kv_heads,
@@ -407,6 +434,7 @@ TORCH_LIBRARY(atta, m) {
   m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rms_norm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
+  m.def("embed(Tensor(a!) out, Tensor table, Tensor ids, Tensor? prev, Tensor? feed_prev) -> ()");
   m.def(
       "rope_cache(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor qkv, "
       "Tensor positions, Tensor slot_mapping, Tensor cos_sin, int n_q_heads, int n_kv_heads, "
@@ -428,6 +456,7 @@ TORCH_LIBRARY_IMPL(atta, CUDA, m) {
   m.impl("rms_norm", &rms_norm);
   m.impl("fused_add_rms_norm", &fused_add_rms_norm);
   m.impl("silu_and_mul", &silu_and_mul);
+  m.impl("embed", &embed);
   m.impl("rope_cache", &rope_cache);
   m.impl("attention_prefill", &attention_prefill);
   m.impl("attention_decode", &attention_decode);

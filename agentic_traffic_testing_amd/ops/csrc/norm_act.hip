@@ -94,9 +94,38 @@ __global__ __launch_bounds__(256) void silu_and_mul_kernel(uint16_t* __restrict_
   }
 }
 
+// Token-embedding gather.  One workgroup per row, 16-byte copies.  Row r
+// takes token ids[r], or prev[r] when *feed_prev != 0: an async-decode look-ahead step is
+// enqueued before the host has read the previous step's samples, so it reads its input
+// tokens straight from the sampler's device output (engine/llm_engine.py).
+__global__ __launch_bounds__(256) void embed_kernel(uint16_t* __restrict__ out,
+                                                    const uint16_t* __restrict__ table,
+                                                    const int* __restrict__ ids,
+                                                    const int64_t* __restrict__ prev,
+                                                    const int* __restrict__ feed_prev, int hidden,
+                                                    int64_t vocab, int64_t out_stride) {
+  const int64_t row = blockIdx.x;
+  int64_t tok = (feed_prev != nullptr && feed_prev[0] != 0) ? prev[row] : ids[row];
+  tok = tok < 0 ? 0 : (tok >= vocab ? vocab - 1 : tok);
+  const Pack8* src = reinterpret_cast<const Pack8*>(table + tok * hidden);
+  Pack8* dst = reinterpret_cast<Pack8*>(out + row * out_stride);
+  for (int v = threadIdx.x; v < (hidden >> 3); v += blockDim.x) dst[v] = src[v];
+}
+
 }  // namespace atta
 
 using namespace atta;
+
+int atta_embed(void* out, const void* table, const int* ids, const int64_t* prev,
+               const int* feed_prev, int rows, int hidden, int64_t vocab, int64_t out_stride,
+               hipStream_t stream) {
+  if (hidden % 8 != 0 || out_stride % 8 != 0) return -1;
+  if (rows == 0) return 0;
+  embed_kernel<<<rows, 256, 0, stream>>>(static_cast<uint16_t*>(out),
+                                         static_cast<const uint16_t*>(table), ids, prev,
+                                         feed_prev, hidden, vocab, out_stride);
+  return static_cast<int>(hipGetLastError());
+}
 
 int atta_rms_norm(void* out, void* residual, const void* x, const void* w, int rows, int hidden,
                   int64_t x_stride, int64_t out_stride, int64_t res_stride, float eps, int dtype,

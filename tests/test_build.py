@@ -5,7 +5,7 @@ import torch
 from agentic_traffic_testing_amd.ops import build
 
 EXPECTED_OPS = {
-    "rms_norm", "fused_add_rms_norm", "silu_and_mul", "rope_cache", "attention_prefill",
+    "rms_norm", "fused_add_rms_norm", "silu_and_mul", "embed", "rope_cache", "attention_prefill",
     "attention_decode", "attention_decode_v2", "sample", "skinny_gemm", "fused_qkv_rope",
     "fused_gate_up_silu", "fused_lm_head_sample", "sample_finalize", "skinny_variant",
     "ar_buffer_bytes", "ar_alloc", "ar_free", "ar_handle", "ar_open", "ar_close", "ar_error",
@@ -29,3 +29,16 @@ def test_runtime_extension_loads():
     bm = BlockManager(8, 16, True)
     assert bm.num_free_blocks() == 8
     assert ShmChannel is not None
+
+
+def test_embed_cpu_fallback_honours_lookahead_flag():
+    from agentic_traffic_testing_amd import ops
+
+    table = torch.randn(50, 16)
+    ids = torch.tensor([1, 2, 3], dtype=torch.int32)
+    prev = torch.tensor([7, 8, 9, 10], dtype=torch.int64)
+    assert torch.equal(ops.embed(table, ids), table[[1, 2, 3]])
+    assert torch.equal(ops.embed(table, ids, prev, torch.zeros(1, dtype=torch.int32)),
+                       table[[1, 2, 3]])
+    assert torch.equal(ops.embed(table, ids, prev, torch.ones(1, dtype=torch.int32)),
+                       table[[7, 8, 9]])

@@ -55,6 +55,21 @@ def test_silu_and_mul(dtype, shape):
     close(ops.silu_and_mul(x), ref.silu_and_mul(x), 2e-2, 1e-2)
 
 
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("rows", [1, 5, 16, 300])
+def test_embed(dtype, rows):
+    torch.manual_seed(3)
+    table = torch.randn(1000, 4096, dtype=dtype, device="cuda")
+    ids = torch.randint(0, 1000, (rows,), device="cuda", dtype=torch.int32)
+    close(ops.embed(table, ids), torch.nn.functional.embedding(ids.long(), table), 0.0)
+    # look-ahead mode: the device flag switches the row source to the int64 sample buffer
+    prev = torch.randint(0, 1000, (rows + 3,), device="cuda", dtype=torch.int64)
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    close(ops.embed(table, ids, prev, flag), torch.nn.functional.embedding(ids.long(), table), 0.0)
+    flag.fill_(1)
+    close(ops.embed(table, ids, prev, flag), torch.nn.functional.embedding(prev[:rows], table), 0.0)
+
+
 def _rand_cache(nb, hkv, bs, d, dtype):
     k = torch.randn(nb, hkv, bs, d, dtype=dtype, device="cuda")
     v = torch.randn(nb, hkv, d, bs, dtype=dtype, device="cuda")
