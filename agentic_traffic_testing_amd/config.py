@@ -83,6 +83,18 @@ MODEL_PRESETS: dict[str, ModelConfig] = {
     "small": ModelConfig(name="small", vocab_size=32768, hidden_size=1024, intermediate_size=2816,
                          num_layers=4, num_heads=8, num_kv_heads=2, max_position_embeddings=8192,
                          bos_token_id=32512, eos_token_ids=(32513, 32521)),
+    # TP rehearsal shape: 8 q heads over 2 KV heads, so TP=4/8 replicate KV heads (kv_rep > 1)
+    "tiny-tp8": ModelConfig(name="tiny-tp8", vocab_size=4096, hidden_size=256,
+                            intermediate_size=512, num_layers=2, num_heads=8, num_kv_heads=2,
+                            max_position_embeddings=4096, bos_token_id=3840,
+                            eos_token_ids=(3841, 3849)),
+    # 70B attention geometry (GQA 8:1, hidden 8192) with few layers / a small FFN and vocab:
+    # the G=8 decode path and 8192-wide GEMVs on one GPU in seconds
+    "llama-70b-slice": ModelConfig(name="llama-70b-slice", vocab_size=16384, hidden_size=8192,
+                                   intermediate_size=3584, num_layers=2, num_heads=64,
+                                   num_kv_heads=8, rope_scaling=None,
+                                   max_position_embeddings=16384, bos_token_id=16000,
+                                   eos_token_ids=(16001, 16009)),
 }
 
 
@@ -174,6 +186,9 @@ class EngineConfig:
     tp_same_device: bool = False
     tp_allreduce: str = "auto"           # auto | rccl | ipc (custom one-shot all-reduce)
     dist_port: int = 0                   # 0 = pick a free port
+    # a TP worker that has not registered on the step channel this long after rank 0
+    # created it is reported dead (covers workers that die while loading weights)
+    tp_register_timeout_s: float = 900.0
 
     def replace(self, **kw) -> "EngineConfig":
         return replace(self, **kw)

@@ -154,6 +154,18 @@ class AsyncEngine:
                     self.last_error = f"TP ranks {dead} died\n" + self.last_error
                     self._fail_pending(RuntimeError(f"engine dead: TP ranks {dead} died"))
                     return
+                if getattr(eng, "step_failure_fatal", False):
+                    # TP: rank 0 may already have published this step, so the workers are
+                    # inside collectives rank 0 will never join - any later collective would
+                    # pair with the wrong step.  Stop the whole TP group; /health -> 503.
+                    self.last_error = "TP step failed after publish; engine stopped\n" + \
+                        self.last_error
+                    self._fail_pending(RuntimeError("engine dead: TP step failed"))
+                    try:
+                        eng.kill()
+                    except Exception:
+                        pass
+                    return
                 continue
             for o in outs:
                 self._deliver(o.request_id, o)

@@ -24,16 +24,35 @@ class NativeKernelsUnavailable(RuntimeError):
     pass
 
 
+def library_build_hash(path: Path = _LIB) -> str | None:
+    """Source hash embedded in a built kernel library (ops/build.py), or None."""
+    import ctypes
+
+    try:
+        fn = ctypes.CDLL(str(path)).atta_build_hash
+    except (OSError, AttributeError):
+        return None
+    fn.restype = ctypes.c_char_p
+    return fn().decode()
+
+
 def load_native(build_if_missing: bool = True) -> bool:
-    """Load the HIP kernel library (building it in-tree first if needed)."""
+    """Load the HIP kernel library.  With ``build_if_missing`` the library is (re)built
+    in-tree when missing or when its sources changed (content-hash stamps); without it a
+    library whose embedded source hash does not match the sources is refused."""
     global _loaded, _load_error
     if _loaded:
         return True
     try:
-        if not _LIB.exists() and build_if_missing:
-            from .build import build_kernels
+        from . import build
 
-            build_kernels()
+        if build_if_missing:
+            build.build_kernels()  # no-op when every stamp matches
+        want = build.kernel_source_hash()
+        got = library_build_hash()
+        if got != want:
+            raise RuntimeError(f"stale kernel library {_LIB}: built from sources {got}, "
+                               f"tree has {want}")
         torch.ops.load_library(str(_LIB))
         _loaded = True
         _load_error = None

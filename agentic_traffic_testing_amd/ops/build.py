@@ -4,11 +4,19 @@ Produces, next to the sources (so the .so files travel with a gpurun snapshot):
 
 * ``ops/_atta_kernels.so``  - CDNA4 HIP kernels + torch operator registration
   (``torch.ops.atta.*``), compiled with ``hipcc --offload-arch=gfx950``.
-* ``runtime/_atta_runtime*.so`` - C++ block manager / batch builder (pybind11, g++).
+* ``runtime/_atta_runtime*.so`` - C++ block manager / batch builder / TP step channel
+  (pybind11, g++).
 
 No torch.utils.cpp_extension / hipify: sources are plain HIP written for CDNA4 and are
-compiled with explicit hipcc command lines.  Builds are incremental (mtime based) and
-parallel.
+compiled with explicit hipcc command lines.
+
+Staleness is decided by CONTENT, not mtimes: every object has a ``.stamp`` holding the
+sha256 of its compile command plus the bytes of its source and of every header in its
+directory, and each library embeds the hash of all its sources (``atta_build_hash()`` in
+the kernel library, ``BUILD_HASH`` in the runtime module).  The loaders
+(``ops.load_native`` / ``runtime._load``) compare that hash against the sources on disk
+and refuse a stale library, so a snapshot whose sources moved on without a rebuild fails
+loudly instead of running old kernels.
 
 Usage:  python -m agentic_traffic_testing_amd.ops.build [--force] [-j N]
 """
@@ -16,6 +24,7 @@ from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
+import hashlib
 import os
 import shutil
 import subprocess
@@ -43,11 +52,45 @@ def _torch_paths():
     return ce.include_paths(), ce.library_paths()
 
 
-def _stale(target: Path, deps) -> bool:
-    if not target.exists():
-        return True
-    t = target.stat().st_mtime
-    return any(Path(d).stat().st_mtime > t for d in deps)
+def _sha(parts) -> str:
+    h = hashlib.sha256()
+    for p in parts:
+        h.update(p if isinstance(p, bytes) else str(p).encode())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def _files_digest(files) -> list:
+    out = []
+    for f in sorted(Path(x) for x in files):
+        out += [f.name, f.read_bytes()]
+    return out
+
+
+def kernel_sources() -> list[Path]:
+    return sorted([*CSRC.glob("*.hip"), *CSRC.glob("*.h"), *CSRC.glob("*.cpp")])
+
+
+def runtime_sources() -> list[Path]:
+    return sorted([*RUNTIME_CSRC.glob("*.cpp"), *RUNTIME_CSRC.glob("*.h")])
+
+
+def kernel_source_hash() -> str:
+    """Hash of every kernel-library source (what ``atta_build_hash()`` must return)."""
+    return _sha(["kernels", ARCH, *_files_digest(kernel_sources())])[:32]
+
+
+def runtime_source_hash() -> str:
+    return _sha(["runtime", *_files_digest(runtime_sources())])[:32]
+
+
+def _stamp_ok(target: Path, digest: str) -> bool:
+    st = target.with_name(target.name + ".stamp")
+    return target.exists() and st.exists() and st.read_text().strip() == digest
+
+
+def _write_stamp(target: Path, digest: str):
+    target.with_name(target.name + ".stamp").write_text(digest + "\n")
 
 
 def _run(cmd):
@@ -59,41 +102,59 @@ def _run(cmd):
 
 def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> Path:
     BUILD.mkdir(parents=True, exist_ok=True)
-    headers = list(CSRC.glob("*.h"))
-    hip_srcs = sorted(CSRC.glob("*.hip"))
+    headers = sorted(CSRC.glob("*.h"))
+    hdr_digest = _files_digest(headers)
+    src_hash = kernel_source_hash()
+    # the library's identity: generated translation unit returning the source hash
+    info = BUILD / "build_info.cpp"
+    info_src = (f'extern "C" const char* atta_build_hash() {{ return "{src_hash}"; }}\n')
+    if not info.exists() or info.read_text() != info_src:
+        info.write_text(info_src)
+    jobs_ = []  # (cmd, obj, digest)
     objs = []
-    cmds = []
-    for src in hip_srcs:
+    for src in sorted(CSRC.glob("*.hip")):
         obj = BUILD / (src.stem + ".o")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+               "-munsafe-fp-atomics", "-Wno-unused-result", "-I", str(CSRC),
+               "-c", str(src), "-o", str(obj)]
         objs.append(obj)
-        if force or _stale(obj, [src, *headers]):
-            cmds.append([
-                HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-                "-munsafe-fp-atomics", "-Wno-unused-result", "-I", str(CSRC),
-                "-c", str(src), "-o", str(obj),
-            ])
+        jobs_.append((cmd, obj, _sha([*cmd, src.read_bytes(), *hdr_digest])))
     inc, libdirs = _torch_paths()
     bind_src = CSRC / "bindings.cpp"
     bind_obj = BUILD / "bindings.o"
+    cmd = [HIPCC, "-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__=1",
+           "-DUSE_ROCM=1", "-D_GLIBCXX_USE_CXX11_ABI=1", "-Wno-unused-result",
+           "-Wno-deprecated-declarations", "-I", str(CSRC)]
+    for i in inc:
+        cmd += ["-I", i]
+    cmd += ["-c", str(bind_src), "-o", str(bind_obj)]
     objs.append(bind_obj)
-    if force or _stale(bind_obj, [bind_src, *headers]):
-        cmd = [HIPCC, "-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__=1",
-               "-DUSE_ROCM=1", "-D_GLIBCXX_USE_CXX11_ABI=1", "-Wno-unused-result",
-               "-Wno-deprecated-declarations", "-I", str(CSRC)]
-        for i in inc:
-            cmd += ["-I", i]
-        cmd += ["-c", str(bind_src), "-o", str(bind_obj)]
-        cmds.append(cmd)
+    jobs_.append((cmd, bind_obj, _sha([*cmd, bind_src.read_bytes(), *hdr_digest])))
+    info_obj = BUILD / "build_info.o"
+    cmd = ["g++", "-O2", "-fPIC", "-c", str(info), "-o", str(info_obj)]
+    objs.append(info_obj)
+    jobs_.append((cmd, info_obj, _sha([*cmd, info_src])))
+    todo = [j for j in jobs_ if force or not _stamp_ok(j[1], j[2])]
+
+    def compile_one(j):
+        cmd_, obj_, dig = j
+        r = _run(cmd_)
+        _write_stamp(obj_, dig)
+        return r
+
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        for r in ex.map(_run, cmds):
+        for r in ex.map(compile_one, todo):
             if verbose and (r.stdout or r.stderr):
                 print(r.stdout, r.stderr)
-    if force or cmds or _stale(KERNEL_SO, objs):
-        link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(KERNEL_SO), *map(str, objs)]
-        for d in libdirs:
-            link += ["-L", d, f"-Wl,-rpath,{d}"]
-        link += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip"]
+    link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(KERNEL_SO),
+            *map(str, objs)]
+    for d in libdirs:
+        link += ["-L", d, f"-Wl,-rpath,{d}"]
+    link += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip"]
+    link_digest = _sha([*link, *(j[2] for j in jobs_)])
+    if force or todo or not _stamp_ok(KERNEL_SO, link_digest):
         _run(link)
+        _write_stamp(KERNEL_SO, link_digest)
     return KERNEL_SO
 
 
@@ -102,20 +163,25 @@ def runtime_so_path() -> Path:
     return RUNTIME_DIR / f"_atta_runtime{suffix}"
 
 
-def build_runtime(force: bool = False) -> Path:
+def runtime_flags(extra=()) -> list[str]:
     import pybind11
 
+    py_inc = sysconfig.get_paths()["include"]
+    return ["-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", *extra,
+            "-I", pybind11.get_include(), "-I", py_inc, "-I", str(RUNTIME_CSRC),
+            f'-DATTA_BUILD_HASH="{runtime_source_hash()}"']
+
+
+def build_runtime(force: bool = False) -> Path:
     target = runtime_so_path()
     srcs = sorted(RUNTIME_CSRC.glob("*.cpp"))
-    hdrs = sorted(RUNTIME_CSRC.glob("*.h"))
     if not srcs:
         raise RuntimeError("no runtime sources")
-    if force or _stale(target, [*srcs, *hdrs]):
-        py_inc = sysconfig.get_paths()["include"]
-        cmd = ["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall", "-Wno-unused-function",
-               "-I", pybind11.get_include(), "-I", py_inc, "-I", str(RUNTIME_CSRC),
-               *map(str, srcs), "-o", str(target)]
+    cmd = ["g++", "-O3", "-shared", *runtime_flags(), *map(str, srcs), "-o", str(target)]
+    digest = _sha([*cmd, *_files_digest(runtime_sources())])
+    if force or not _stamp_ok(target, digest):
         _run(cmd)
+        _write_stamp(target, digest)
     return target
 
 

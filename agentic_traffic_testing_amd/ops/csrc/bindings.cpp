@@ -74,11 +74,24 @@ void embed(at::Tensor out, const at::Tensor& table, const at::Tensor& ids,
   TORCH_CHECK(ids.scalar_type() == at::kInt && ids.is_contiguous() && ids.numel() >= out.size(0),
               "embed: ids int32 [T]");
   TORCH_CHECK(out.scalar_type() == table.scalar_type(), "embed: dtype");
+  check_dev(ids, "ids");
+  check_dev(out, "out");
+  TORCH_CHECK(ids.device() == table.device() && out.device() == table.device(),
+              "embed: tensors on different devices");
+  // the kernel moves rows with 16-byte loads/stores
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(table.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0 &&
+                  (table.size(1) * table.element_size()) % 16 == 0 &&
+                  (out.stride(0) * out.element_size()) % 16 == 0,
+              "embed: table/out rows must be 16-byte aligned");
   const int64_t* pv = nullptr;
   const int* fp = nullptr;
   if (feed_prev.has_value()) {
     TORCH_CHECK(prev.has_value() && prev->scalar_type() == at::kLong && prev->is_contiguous(),
                 "embed: prev int64");
+    check_dev(*prev, "prev");
+    check_dev(*feed_prev, "feed_prev");
+    TORCH_CHECK(prev->numel() >= out.size(0), "embed: prev shorter than the output rows");
     TORCH_CHECK(feed_prev->scalar_type() == at::kInt && feed_prev->numel() >= 1, "embed: flag");
     pv = prev->data_ptr<int64_t>();
     fp = feed_prev->data_ptr<int>();

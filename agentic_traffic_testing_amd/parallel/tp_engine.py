@@ -133,13 +133,45 @@ class TPEngine(LLMEngine):
         _maybe_ipc(cfg, comm, runner)
         from ..runtime import ShmChannel
 
-        # workers poll for the channel after their own (identical) runner init
+        # workers poll for the channel after their own (identical) runner init; a worker
+        # that has not registered within tp_register_timeout_s counts as dead (it died
+        # before it could register, e.g. out of memory while loading its shard)
         self.channel = ShmChannel(channel_name(port), HDR_WORDS + runner.max_layout.size,
-                                  world - 1, create=True)
+                                  world - 1, create=True,
+                                  register_timeout_s=cfg.tp_register_timeout_s)
         runner.publisher = self.channel
         super().__init__(cfg, runner=runner, device=device)
-        runner.capture_all()
         self._closed = False
+        try:
+            runner.capture_all()
+        except BaseException:
+            self.kill()
+            raise
+
+    # a step that raises after rank 0 published it leaves the workers inside collectives
+    # rank 0 never joins: the serving loop must stop the group instead of continuing
+    step_failure_fatal = True
+
+    def kill(self):
+        """Stop the TP group without the stop handshake (used after a failed step):
+        close the step channel so idle workers exit, terminate spawned workers that are
+        stuck in a collective, and tear down the process group."""
+        if getattr(self, "_closed", True):
+            return
+        self._closed = True
+        ch = getattr(self, "channel", None)
+        if ch is not None:
+            ch.close()
+        for p in self.procs:
+            p.join(timeout=2)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+        try:
+            if torch.distributed.is_initialized():
+                torch.distributed.destroy_process_group()
+        except Exception:
+            pass
 
     def dead_ranks(self) -> list[int]:
         """TP ranks whose process is gone (spawned children, or torchrun peers that had

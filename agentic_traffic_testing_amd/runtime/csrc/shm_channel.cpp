@@ -49,6 +49,10 @@ struct alignas(64) Header {
   uint32_t capacity;   // int32 words per slot
   uint32_t n_readers;
   int32_t writer_pid;
+  // CLOCK_MONOTONIC (system-wide) deadline by which every reader must have registered; a
+  // reader still unregistered after it counts as dead (e.g. a worker that died while
+  // loading weights, before register_reader).  0 = no deadline.
+  int64_t register_deadline_ns;
   alignas(64) std::atomic<uint64_t> seq;
   alignas(64) std::atomic<uint32_t> closed;
   alignas(64) std::atomic<uint64_t> acks[kMaxReaders];
@@ -59,6 +63,12 @@ struct alignas(64) Header {
 // true unless `pid` provably no longer exists (EPERM: alive but not ours)
 inline bool pid_alive(int32_t pid) {
   return pid <= 0 || kill(static_cast<pid_t>(pid), 0) == 0 || errno != ESRCH;
+}
+
+inline int64_t mono_ns() {
+  timespec ts{};
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<int64_t>(ts.tv_sec) * 1000000000ll + ts.tv_nsec;
 }
 
 inline void cpu_relax() { __builtin_ia32_pause(); }
@@ -76,7 +86,8 @@ inline void backoff(uint64_t& spins) {
 
 class ShmChannel {
  public:
-  ShmChannel(const std::string& name, int64_t capacity_words, int n_readers, bool create)
+  ShmChannel(const std::string& name, int64_t capacity_words, int n_readers, bool create,
+             double register_timeout_s)
       : name_(name.empty() || name[0] != '/' ? "/" + name : name), owner_(create) {
     if (n_readers < 0 || n_readers > kMaxReaders) throw std::invalid_argument("n_readers");
     int fd = -1;
@@ -109,6 +120,10 @@ class ShmChannel {
       hdr_->capacity = static_cast<uint32_t>(capacity_words);
       hdr_->n_readers = static_cast<uint32_t>(n_readers);
       hdr_->writer_pid = static_cast<int32_t>(getpid());
+      hdr_->register_deadline_ns =
+          register_timeout_s > 0
+              ? mono_ns() + static_cast<int64_t>(register_timeout_s * 1e9)
+              : 0;
       for (auto& r : hdr_->reader_pids) r.store(0, std::memory_order_relaxed);
       hdr_->seq.store(0, std::memory_order_relaxed);
       hdr_->closed.store(0, std::memory_order_relaxed);
@@ -138,11 +153,20 @@ class ShmChannel {
     hdr_->reader_pids[reader].store(static_cast<int32_t>(getpid()), std::memory_order_release);
   }
 
-  // Reader ids whose registered process no longer exists.
+  // Reader ids whose registered process no longer exists, or that never registered before
+  // the registration deadline.
   py::list dead_readers() const {
     py::list out;
     for (uint32_t r = 0; r < hdr_->n_readers; ++r)
-      if (!pid_alive(hdr_->reader_pids[r].load(std::memory_order_acquire))) out.append(r);
+      if (reader_dead(r)) out.append(r);
+    return out;
+  }
+
+  // Reader ids that have not registered yet.
+  py::list unregistered_readers() const {
+    py::list out;
+    for (uint32_t r = 0; r < hdr_->n_readers; ++r)
+      if (hdr_->reader_pids[r].load(std::memory_order_acquire) == 0) out.append(r);
     return out;
   }
 
@@ -216,6 +240,13 @@ class ShmChannel {
       throw std::out_of_range("reader id");
   }
 
+  bool reader_dead(uint32_t r) const {
+    const int32_t pid = hdr_->reader_pids[r].load(std::memory_order_acquire);
+    if (pid == 0)
+      return hdr_->register_deadline_ns > 0 && mono_ns() > hdr_->register_deadline_ns;
+    return !pid_alive(pid);
+  }
+
   // 0: every reader acknowledged `target`; -1: timeout; r + 1: reader r's process is gone.
   int wait_acks(uint64_t target, double timeout_s) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -223,8 +254,7 @@ class ShmChannel {
     for (uint32_t r = 0; r < hdr_->n_readers; ++r) {
       while (hdr_->acks[r].load(std::memory_order_acquire) < target) {
         if ((spins & 1023) == 1023) {
-          if (!pid_alive(hdr_->reader_pids[r].load(std::memory_order_acquire)))
-            return static_cast<int>(r) + 1;
+          if (reader_dead(r)) return static_cast<int>(r) + 1;
           if (timeout_s >= 0) {
             const double el =
                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -248,8 +278,9 @@ class ShmChannel {
 
 void register_shm_channel(py::module_& m) {
   py::class_<ShmChannel>(m, "ShmChannel")
-      .def(py::init<const std::string&, int64_t, int, bool>(), py::arg("name"),
-           py::arg("capacity_words") = 0, py::arg("n_readers") = 0, py::arg("create") = false)
+      .def(py::init<const std::string&, int64_t, int, bool, double>(), py::arg("name"),
+           py::arg("capacity_words") = 0, py::arg("n_readers") = 0, py::arg("create") = false,
+           py::arg("register_timeout_s") = 0.0)
       .def_property_readonly("capacity", &ShmChannel::capacity)
       .def_property_readonly("n_readers", &ShmChannel::n_readers)
       .def_property_readonly("seq", &ShmChannel::seq)
@@ -257,6 +288,7 @@ void register_shm_channel(py::module_& m) {
       .def_property_readonly("writer_alive", &ShmChannel::writer_alive)
       .def("register_reader", &ShmChannel::register_reader, py::arg("reader"))
       .def("dead_readers", &ShmChannel::dead_readers)
+      .def("unregistered_readers", &ShmChannel::unregistered_readers)
       .def("publish", &ShmChannel::publish, py::arg("data"), py::arg("timeout_s") = -1.0)
       .def("receive", &ShmChannel::receive, py::arg("reader"), py::arg("last_seq"),
            py::arg("timeout_s") = -1.0)

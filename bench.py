@@ -4,17 +4,25 @@ Llama-3-8B (3.1 shape) bf16, TP=1 per engine (BASELINE.json).
 
 One timed *step* = one fan-out episode per rank (agentic_traffic_testing_amd/bench/fanout.py):
 planning request -> 5 concurrent Agent-B requests -> final synthesis request, each
-generating exactly ``--max-tokens`` (512) tokens with temperature 0.2.  With N GPUs
-(``torch.distributed.run --nproc-per-node N``) every rank is an independent engine replica
-(data-parallel serving, weak scaling) on its own GPU; the reported value is the whole-job
-completion tokens/s (sum over ranks / slowest rank's wall time).
+generating exactly ``--max-tokens`` (512) tokens with temperature 0.2.
 
-``--parallel tp`` instead runs ONE engine tensor-parallel over the N ranks (rank 0 drives the
-workload; the other ranks replay its steps, parallel/tp_engine.py) - the TP scaling curve
-BASELINE.md asks for next to the replica (dp) curve; that mode is strong scaling.
+Multi-GPU (one process per GPU):
 
-Weights are seeded random-init of the exact Llama-3.1-8B architecture and prompts are
-synthetic (no network / gated checkpoints), which ``data`` states.
+* ``python bench.py --gpus N`` launches the N ranks ITSELF: it starts
+  ``python -m torch.distributed.run --nproc-per-node N`` as a child process (before this
+  process touches the GPU; it only counts devices) and exits with the child's status.
+  Under an external ``torch.distributed.run`` (WORLD_SIZE set) ``--gpus`` must equal
+  WORLD_SIZE.  N larger than the visible GPU count is an error, not a silent N=1 run.
+* ``--parallel dp`` (default): every rank is an independent engine replica on its own GPU
+  (data-parallel serving, weak scaling); the value is whole-job completion tokens/s (sum
+  over ranks / slowest rank's wall time), with the per-rank rates listed too.
+* ``--parallel tp``: ONE engine tensor-parallel over the N ranks (rank 0 drives the
+  workload; the other ranks replay its steps, parallel/tp_engine.py) - strong scaling.
+
+Weights are seeded random-init of the exact Llama-3.1-8B architecture (``--model
+llama-3-70b`` for BASELINE configs 4/5) and prompts are synthetic (no network / gated
+checkpoints), which ``data`` states.  ``--device cpu`` runs the same protocol on the CPU
+(gloo, tiny models) for the CPU test tier.
 
 Prints ONE JSON line on rank 0.
 """
@@ -23,16 +31,20 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
 
 METRIC = "llm-backend tokens/sec + p50 TTFT under 5-agent fan-out, Llama-3-8B TP=1"
-
+DATA = ("synthetic (agent fan-out prompts, synthetic tokenizer, seeded random-init {} "
+        "weights)")
 
 
 def overrides(items: list[str]) -> dict:
@@ -51,7 +63,8 @@ def overrides(items: list[str]) -> dict:
         out[k] = (v.lower() in ("1", "true", "yes")) if t is bool else t(v)
     return out
 
-def main():
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -64,6 +77,8 @@ def main():
     ap.add_argument("--max-num-batched-tokens", type=int, default=8192)
     ap.add_argument("--gpu-memory-utilization", type=float, default=0.90)
     ap.add_argument("--dtype", default="bfloat16")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu: CPU-tier rehearsal of the protocol (gloo, tiny models)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--quantization", default="", choices=["", "fp8"],
@@ -72,33 +87,92 @@ def main():
                     help="EngineConfig override for A/B runs (e.g. fuse_attn_oproj=0)")
     ap.add_argument("--parallel", choices=["dp", "tp"], default="dp",
                     help="dp: one engine replica per GPU (default); tp: one engine over all GPUs")
-    a = ap.parse_args()
-    if a.parallel == "tp" and int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        return main_tp(a)
+    return ap.parse_args(argv)
 
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(a) -> int:
+    """Start N ranks under torch.distributed.run as a CHILD process and return its status.
+
+    Runs before this process makes any GPU call (device_count() does not initialise HIP on
+    this image), so no exec happens from a GPU-initialised process."""
+    if a.device == "cuda":
+        have = torch.cuda.device_count()
+        if have < a.gpus:
+            print(json.dumps({"metric": METRIC, "error": f"--gpus {a.gpus} requested but only "
+                              f"{have} GPU(s) visible", "n_gpus": a.gpus}), flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", ATTA_BENCH_CHILD="1")
+    return subprocess.call(cmd, env=env)
+
+
+def main(argv=None):
+    a = parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(a)
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} does not match WORLD_SIZE {world}")
+    if a.parallel == "tp" and world > 1:
+        return main_tp(a)
+    return main_dp(a, world)
+
+
+def _cfg(a, device: str, **kw):
+    from agentic_traffic_testing_amd.config import EngineConfig
+
+    base = dict(model=a.model, dtype=a.dtype, max_model_len=a.max_model_len,
+                max_num_seqs=a.max_num_seqs, max_num_batched_tokens=a.max_num_batched_tokens,
+                gpu_memory_utilization=a.gpu_memory_utilization,
+                use_graphs=not a.no_graphs and a.device == "cuda", seed=1234, device=device,
+                quantization=a.quantization)
+    base.update(kw)
+    base.update(overrides(a.set))
+    return EngineConfig(**base)
+
+
+def _model_label(a) -> str:
+    from agentic_traffic_testing_amd.config import resolve_model
+
+    return resolve_model(a.model)[0].name
+
+
+def _sync(a):
+    if a.device == "cuda":
+        torch.cuda.synchronize()
+
+
+def main_dp(a, world: int):
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    cuda = a.device == "cuda"
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    else:
+        if cuda:
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo")
+    elif cuda:
         torch.cuda.set_device(0)
-    dev = f"cuda:{torch.cuda.current_device()}"
+    dev = f"cuda:{torch.cuda.current_device()}" if cuda else "cpu"
 
     from agentic_traffic_testing_amd.bench.fanout import FanoutWorkload
-    from agentic_traffic_testing_amd.config import EngineConfig
     from agentic_traffic_testing_amd.engine.llm_engine import LLMEngine
 
-    cfg = EngineConfig(model=a.model, dtype=a.dtype, max_model_len=a.max_model_len,
-                       max_num_seqs=a.max_num_seqs,
-                       max_num_batched_tokens=a.max_num_batched_tokens,
-                       gpu_memory_utilization=a.gpu_memory_utilization,
-                       use_graphs=not a.no_graphs, seed=1234, device=dev,
-                       quantization=a.quantization, **overrides(a.set))
+    cfg = _cfg(a, dev)
     t0 = time.perf_counter()
     eng = LLMEngine(cfg)
     eng.runner.capture_all()
@@ -116,18 +190,19 @@ def main():
 
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync(a)
     t_start = time.perf_counter()
     results = [wl.run_episode() for _ in range(a.steps)]
-    torch.cuda.synchronize()
+    _sync(a)
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
 
     if a.verbose and rank == 0:
-        tm, rt = eng.timing, eng.runner.timing
+        tm = eng.timing
         n = max(1, tm["steps"])
         g = max(1, eng.runner.graph_steps)
+        rt = eng.runner.timing
         log(f"host step breakdown over {n} steps: schedule {tm['schedule'] / n * 1e3:.3f} ms, "
             f"execute {tm['execute'] / n * 1e3:.3f} ms, post {tm['post'] / n * 1e3:.3f} ms; "
             f"graph steps {eng.runner.graph_steps}: prep {rt['graph_prep'] / g * 1e3:.3f} ms, "
@@ -135,22 +210,22 @@ def main():
     tokens = sum(r.completion_tokens for r in results)
     ttfts = [t for r in results for t in r.ttfts]
     lat = [t for r in results for t in r.latencies]
-    stats = torch.tensor([elapsed, float(tokens)], dtype=torch.float64, device=dev)
+    per_rank = [round(tokens / elapsed, 2)]
     if dist:
-        t_max = stats[0:1].clone()
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        tok_sum = stats[1:2].clone()
-        dist.all_reduce(tok_sum, op=dist.ReduceOp.SUM)
-        all_ttft = [None] * world
-        dist.all_gather_object(all_ttft, ttfts)
-        ttfts = [t for lst in all_ttft for t in lst]
-        elapsed, tokens = float(t_max.item()), float(tok_sum.item())
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (elapsed, tokens, ttfts, lat))
+        elapsed = max(g[0] for g in gathered)
+        tokens = sum(g[1] for g in gathered)
+        per_rank = [round(g[1] / g[0], 2) for g in gathered]
+        ttfts = [t for g in gathered for t in g[2]]
+        lat = [t for g in gathered for t in g[3]]
     value = tokens / elapsed
     if rank == 0:
         ms = elapsed / a.steps * 1000.0
-        p50 = statistics.median(ttfts) if ttfts else None
         srt = sorted(ttfts)
+        p50 = statistics.median(srt) if srt else None
         p95 = srt[min(len(srt) - 1, int(0.95 * len(srt)))] if srt else None
+        label = _model_label(a)
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -163,11 +238,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16" if "bf" in a.dtype else a.dtype,
-            "weights": a.quantization or "bf16",
-            "data": "synthetic (agent fan-out prompts, synthetic tokenizer, seeded random-init "
-                    "Llama-3.1-8B weights)",
+            "weights": a.quantization or ("bf16" if "bf" in a.dtype else a.dtype),
+            "data": DATA.format(label),
             "config": {
-                "model": "Llama-3.1-8B (random-init)",
+                "model": f"{label} (random-init)",
                 "global_batch": a.fanout * world,
                 "seq_len": a.max_model_len,
                 "parallelism": f"dp{world}" if world > 1 else "tp1",
@@ -176,8 +250,10 @@ def main():
                 "max_num_batched_tokens": a.max_num_batched_tokens,
                 "block_size": cfg.block_size,
                 "temperature": 0.2,
-                "hipgraphs": not a.no_graphs,
+                "hipgraphs": cfg.use_graphs,
+                "device": a.device,
             },
+            "per_rank_tokens_per_s": per_rank,
             "p50_ttft_s": round(p50, 4) if p50 is not None else None,
             "p95_ttft_s": round(p95, 4) if p95 is not None else None,
             "p50_latency_s": round(statistics.median(lat), 3) if lat else None,
@@ -189,59 +265,62 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 def main_tp(a):
     """Tensor-parallel bench: ranks > 0 serve rank 0's steps until it stops them."""
     world = int(os.environ["WORLD_SIZE"])
     rank = int(os.environ.get("RANK", "0"))
-    from agentic_traffic_testing_amd.config import EngineConfig
-
-    cfg = EngineConfig(model=a.model, dtype=a.dtype, max_model_len=a.max_model_len,
-                       max_num_seqs=a.max_num_seqs,
-                       max_num_batched_tokens=a.max_num_batched_tokens,
-                       gpu_memory_utilization=a.gpu_memory_utilization,
-                       use_graphs=not a.no_graphs, seed=1234, device="cuda",
-                       tensor_parallel_size=world, quantization=a.quantization,
-                       **overrides(a.set))
+    dev = "cuda" if a.device == "cuda" else "cpu"
+    cfg = _cfg(a, dev, tensor_parallel_size=world)
     port = int(os.environ.get("MASTER_PORT", "29511"))
     if rank > 0:
         from agentic_traffic_testing_amd.parallel.tp_engine import run_worker
 
         run_worker(cfg, rank, world, port)
-        return
+        return 0
     from agentic_traffic_testing_amd.bench.fanout import FanoutWorkload
     from agentic_traffic_testing_amd.parallel.tp_engine import TPEngine
 
     t0 = time.perf_counter()
     eng = TPEngine(cfg, external=True)
     init_s = time.perf_counter() - t0
-    wl = FanoutWorkload(eng, fanout=a.fanout, max_tokens=a.max_tokens, seed=0)
-    for _ in range(a.warmup):
-        wl.run_episode()
-    eng.runner.barrier()
-    t_start = time.perf_counter()
-    results = [wl.run_episode() for _ in range(a.steps)]
-    eng.runner.barrier()
-    elapsed = time.perf_counter() - t_start
+    try:
+        wl = FanoutWorkload(eng, fanout=a.fanout, max_tokens=a.max_tokens, seed=0)
+        for _ in range(a.warmup):
+            wl.run_episode()
+        eng.runner.barrier()
+        t_start = time.perf_counter()
+        results = [wl.run_episode() for _ in range(a.steps)]
+        eng.runner.barrier()
+        elapsed = time.perf_counter() - t_start
+    except BaseException:
+        eng.shutdown()
+        raise
     tokens = sum(r.completion_tokens for r in results)
     ttfts = sorted(t for r in results for t in r.ttfts)
+    label = _model_label(a)
     out = {
         "metric": METRIC, "value": round(tokens / elapsed, 2), "unit": "tokens/s",
         "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1000.0, 2), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "bf16" if "bf" in a.dtype else a.dtype,
-        "data": "synthetic (agent fan-out prompts, synthetic tokenizer, seeded random-init "
-                "Llama-3.1-8B weights)",
-        "config": {"model": "Llama-3.1-8B (random-init)", "global_batch": a.fanout,
+        "weights": a.quantization or ("bf16" if "bf" in a.dtype else a.dtype),
+        "data": DATA.format(label),
+        "config": {"model": f"{label} (random-init)", "global_batch": a.fanout,
                    "seq_len": a.max_model_len, "parallelism": f"tp{world}",
-                   "max_tokens": a.max_tokens, "hipgraphs": not a.no_graphs},
+                   "max_tokens": a.max_tokens, "hipgraphs": cfg.use_graphs,
+                   "tp_allreduce": cfg.tp_allreduce, "device": a.device},
         "p50_ttft_s": round(statistics.median(ttfts), 4) if ttfts else None,
+        "p95_ttft_s": round(ttfts[min(len(ttfts) - 1, int(0.95 * len(ttfts)))], 4)
+        if ttfts else None,
         "completion_tokens": int(tokens), "init_s": round(init_s, 1),
     }
     print(json.dumps(out), flush=True)
     eng.shutdown()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

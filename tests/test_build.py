@@ -42,3 +42,27 @@ def test_embed_cpu_fallback_honours_lookahead_flag():
                        table[[1, 2, 3]])
     assert torch.equal(ops.embed(table, ids, prev, torch.ones(1, dtype=torch.int32)),
                        table[[7, 8, 9]])
+
+
+def test_build_is_content_hashed(tmp_path, monkeypatch):
+    """Staleness is decided by source CONTENT: the built library embeds the hash of the
+    sources it came from, and any source edit changes the hash the loader expects."""
+    import shutil
+
+    from agentic_traffic_testing_amd import ops
+
+    build.build_kernels()
+    assert ops.library_build_hash() == build.kernel_source_hash()
+    copy = tmp_path / "csrc"
+    shutil.copytree(build.CSRC, copy)
+    before = build.kernel_source_hash()
+    monkeypatch.setattr(build, "CSRC", copy)
+    assert build.kernel_source_hash() == before  # same bytes, other place/mtime
+    (copy / "common.h").write_text((copy / "common.h").read_text() + "\n// edit\n")
+    assert build.kernel_source_hash() != before
+
+
+def test_runtime_embeds_source_hash():
+    from agentic_traffic_testing_amd import runtime
+
+    assert runtime.BUILD_HASH == build.runtime_source_hash()

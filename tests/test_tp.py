@@ -130,28 +130,99 @@ def _prompts():
     return [rng.integers(300, 3000, size=n).tolist() for n in (33, 9, 70)]
 
 
-def test_tp2_engine_matches_tp1_cpu():
-    base = dict(model="tiny", device="cpu", dtype="float32", max_model_len=256,
+@pytest.mark.parametrize("tp,model", [(2, "tiny"), (4, "tiny-tp8"), (8, "tiny-tp8")])
+def test_tp_engine_matches_tp1_cpu(tp, model):
+    """TP=2/4/8 against TP=1.  tiny-tp8 has 8 q heads over 2 KV heads, so TP=4 and TP=8
+    replicate every KV head over 2 / 4 ranks (kv_rep > 1, models/llama.py)."""
+    base = dict(model=model, device="cpu", dtype="float32", max_model_len=256,
                 num_kv_blocks=64, max_num_batched_tokens=64, max_num_seqs=4, use_graphs=False)
     greedy = SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True)
     sampled = SamplingParams(temperature=0.8, max_tokens=8, ignore_eos=True, seed=11)
     ref_eng = LLMEngine(EngineConfig(**base))
+    n_heads, n_kv, inter = (ref_eng.runner.model.n_heads, ref_eng.runner.model.n_kv_heads,
+                            ref_eng.runner.model.inter)
     exp_g = [o.token_ids for o in ref_eng.generate(_prompts(), greedy)]
     exp_s = [o.token_ids for o in ref_eng.generate(_prompts(), sampled)]
     del ref_eng
-    eng = TPEngine(EngineConfig(tensor_parallel_size=2, **base))
+    eng = TPEngine(EngineConfig(tensor_parallel_size=tp, **base))
     try:
-        assert eng.runner.model.n_heads == 2 and eng.runner.model.inter == 256
+        m = eng.runner.model
+        assert m.n_heads == n_heads // tp and m.inter == inter // tp
+        assert m.kv_rep == max(1, tp // n_kv) and m.n_kv_heads == max(1, n_kv // tp)
         got_g = [o.token_ids for o in eng.generate(_prompts(), greedy)]
         got_s = [o.token_ids for o in eng.generate(_prompts(), sampled)]
-        # top-p path: rank 0 samples, the worker only joins the logits all-gather
-        tp = SamplingParams(temperature=0.7, top_p=0.9, max_tokens=4, ignore_eos=True, seed=3)
-        assert all(len(o.token_ids) == 4 for o in eng.generate(_prompts()[:2], tp))
+        # top-p path: rank 0 samples, the workers only join the logits all-gather
+        topp = SamplingParams(temperature=0.7, top_p=0.9, max_tokens=4, ignore_eos=True, seed=3)
+        assert all(len(o.token_ids) == 4 for o in eng.generate(_prompts()[:2], topp))
     finally:
         eng.shutdown()
     assert got_g == exp_g
     assert got_s == exp_s
     assert not any(p.is_alive() for p in eng.procs)
+
+
+def test_tp_step_failure_stops_the_group():
+    """a step that raises after rank 0 published it must stop the whole TP group
+    (workers exit, the serving loop dies -> /health 503) instead of continuing with ranks
+    whose collectives no longer pair up."""
+    import asyncio
+    import time
+
+    from agentic_traffic_testing_amd.engine.async_engine import AsyncEngine
+
+    base = dict(model="tiny", device="cpu", dtype="float32", max_model_len=256,
+                num_kv_blocks=64, max_num_batched_tokens=64, max_num_seqs=4, use_graphs=False)
+    eng = TPEngine(EngineConfig(tensor_parallel_size=2, **base))
+    runner = eng.runner
+    orig = runner._run
+
+    def failing_run(hdr, sampler=None, worker=False):
+        raise RuntimeError("injected failure after publish")
+
+    runner._run = failing_run
+    ae = AsyncEngine(eng).start()
+    try:
+        async def go():
+            sp = SamplingParams(temperature=0.0, max_tokens=4, ignore_eos=True)
+            with pytest.raises(RuntimeError):
+                async for _ in ae.generate([300, 301, 302], sp, "r0"):
+                    pass
+
+        asyncio.run(go())
+        t0 = time.monotonic()
+        while ae.alive and time.monotonic() - t0 < 30:
+            time.sleep(0.05)
+        assert not ae.alive, "engine loop kept running after a failed TP step"
+        assert "TP step failed" in (ae.last_error or "")
+        for p in eng.procs:
+            p.join(30)
+        assert not any(p.is_alive() for p in eng.procs)
+    finally:
+        runner._run = orig
+        ae._stop.set()
+        eng.kill()
+
+
+def test_shm_channel_registration_deadline():
+    """a reader that never registers (died while loading weights) is reported
+    dead once the registration deadline passes, so rank 0's publish fails instead of
+    blocking forever."""
+    import time
+
+    name = f"atta_pytest_reg_{os.getpid()}"
+    w = ShmChannel(name, 16, 1, create=True, register_timeout_s=0.3)
+    assert w.unregistered_readers() == [0] and w.dead_readers() == []
+    w.publish(np.zeros(1, dtype=np.int32))  # seq 1: nothing to wait for yet
+    time.sleep(0.4)
+    assert w.dead_readers() == [0]
+    with pytest.raises(RuntimeError, match="died"):
+        w.publish(np.zeros(1, dtype=np.int32), 30.0)
+    del w
+    # no deadline (0): an unregistered reader is only slow, never dead
+    w = ShmChannel(name, 16, 1, create=True)
+    w.publish(np.zeros(1, dtype=np.int32))
+    with pytest.raises(RuntimeError, match="in time"):
+        w.publish(np.zeros(1, dtype=np.int32), 0.2)
 
 
 @pytest.mark.gpu
