@@ -172,6 +172,9 @@ class EngineConfig:
     long_prefill_token_threshold: int = 0
     # fused native decode path (GEMV kernels) when available
     fused_decode: bool = True
+    # async look-ahead decode: launch the next decode graph step before waiting for the
+    # current one's tokens (llm_engine.LLMEngine.step)
+    async_decode: bool = True
     # keep a pre-shuffled copy of the decode-GEMV weights (contiguous 1 KiB wave loads)
     preshuffle_decode_weights: bool = True
     # "" = 16-bit weights; "fp8" = OCP e4m3fn weight-only quantisation with per-row scales

@@ -16,9 +16,11 @@ import numpy as np
 
 from ..config import EngineConfig, resolve_model
 from .model_runner import ModelRunner
-from .scheduler import Scheduler
-from .sequence import SamplingParams, Sequence
+from .scheduler import Batch, Scheduler
+from .sequence import SamplingParams, Sequence, SeqStatus
 from .tokenizer import get_tokenizer
+
+PENDING_TOKEN = -1  # output slot of a launched step whose token the host has not seen yet
 
 
 @dataclass
@@ -60,6 +62,14 @@ class StepStats:
     seconds: float
 
 
+@dataclass
+class _Inflight:
+    batch: object
+    handle: dict
+    marks: list      # (seq, output index of this step's token, num_computed after it)
+    t0: float
+
+
 class LLMEngine:
     def __init__(self, cfg: EngineConfig, runner: ModelRunner | None = None, device=None):
         self.cfg = cfg
@@ -78,8 +88,11 @@ class LLMEngine:
         self.batch_size_history: list = []
         # host-side step breakdown (seconds): scheduler, runner.execute (prep + GPU + sync),
         # output processing
-        self.timing = {"schedule": 0.0, "execute": 0.0, "post": 0.0, "steps": 0}
+        self.timing = {"schedule": 0.0, "execute": 0.0, "post": 0.0, "steps": 0,
+                       "lookahead_steps": 0}
         self._rng = random.Random(cfg.seed)
+        # async look-ahead decode: the step launched but not yet collected (see step())
+        self._inflight: _Inflight | None = None
 
     # ------------------------------------------------------------------------------------
     def add_request(self, request_id: str, prompt_ids, sampling: SamplingParams,
@@ -103,19 +116,103 @@ class LLMEngine:
             self.scheduler.abort(request_id)
 
     def has_unfinished(self) -> bool:
-        return self.scheduler.has_work()
+        return self.scheduler.has_work() or self._inflight is not None
 
     # ------------------------------------------------------------------------------------
     def step(self) -> list[RequestOutput]:
+        """One engine step; returns the outputs it produced.
+
+        Async look-ahead decode (``EngineConfig.async_decode``): a decode-only graph step is
+        launched, then - before the host waits for its tokens - the step that continues
+        every one of its sequences is launched too, its input tokens taken on the device
+        from the first step's samples (``ops.embed`` feed_prev path).  The host's scheduling,
+        metadata packing and output processing then overlap the GPU instead of sitting
+        between two replays.  Look-ahead stops (one plain step drains it) whenever requests
+        are waiting for admission, a sequence finishes by length, or the KV pool is full,
+        so outputs are identical to the synchronous engine: a look-ahead token of a sequence
+        that stopped on EOS is discarded."""
         with self.lock:
-            ts = time.perf_counter()
-            batch = self.scheduler.schedule()
-            if batch.empty:
-                return []
-            t0 = time.perf_counter()
+            if self._inflight is None:
+                ts = time.perf_counter()
+                batch = self.scheduler.schedule()
+                if batch.empty:
+                    return []
+                t0 = time.perf_counter()
+                self.timing["schedule"] += t0 - ts
+                if not (self.cfg.async_decode and self.runner.launchable(batch)):
+                    return self._sync_step(batch, t0)
+                self._inflight = self._launch(batch, lookahead=False)
+            cur = self._inflight
+            nxt = self._lookahead_batch(cur)
+            self._inflight = self._launch(nxt, lookahead=True) if nxt is not None else None
+            return self._collect(cur)
+
+    def _launch(self, batch, lookahead: bool) -> "_Inflight":
+        t0 = time.perf_counter()
+        h = self.runner.launch(batch, lookahead=lookahead)  # metadata from pre-step state
+        marks = []
+        for seq in batch.seqs:
+            seq.num_computed += 1
+            marks.append((seq, len(seq.output_ids), seq.num_computed))
+            seq.append(PENDING_TOKEN)  # filled in by _collect
+        if lookahead:
+            self.timing["lookahead_steps"] += 1
+        return _Inflight(batch, h, marks, t0)
+
+    def _lookahead_batch(self, cur: "_Inflight"):
+        """The decode batch continuing ``cur`` row for row, or None to drain."""
+        if not self.cfg.async_decode or self.scheduler.waiting:
+            return None
+        for seq, idx, _ in cur.marks:
+            if seq.status != SeqStatus.RUNNING:
+                return None
+            if idx + 1 >= seq.sampling.max_tokens or \
+                    seq.num_prompt + idx + 1 >= self.cfg.max_model_len:
+                return None  # finishes by length at cur: nothing to look ahead for
+        for seq in cur.batch.seqs:
+            if not self.runner.bm.ensure(seq.seq_id, seq.num_tokens):
+                return None  # KV pool full: the scheduler decides (preemption)
+        n = len(cur.batch.seqs)
+        return Batch(seqs=list(cur.batch.seqs), q_start=[s.num_computed for s in cur.batch.seqs],
+                     q_len=[1] * n, num_decode=n)
+
+    def _collect(self, cur: "_Inflight") -> list[RequestOutput]:
+        toks = self.runner.collect(cur.handle)
+        now = time.perf_counter()
+        self.timing["execute"] += now - cur.t0
+        self.timing["steps"] += 1
+        outs = []
+        for (seq, idx, ncomp), tok in zip(cur.marks, toks):
+            if seq.status == SeqStatus.FINISHED:
+                continue  # aborted while in flight
+            tok = int(tok)
+            seq.output_ids[idx] = tok
+            seq._ids_np = None
+            if seq.first_token_time is None:
+                seq.first_token_time = now
+            self.runner.bm.commit(seq.seq_id, seq.token_array(), ncomp)
+            reason = self._stop_reason(seq, tok, idx + 1)
+            if reason:
+                del seq.output_ids[idx + 1:]  # drop a look-ahead placeholder
+                seq._ids_np = None
+                self.scheduler.finish(seq, reason)
+            outs.append(self._output(seq, [tok], upto=idx + 1))
+        self._account(cur.batch, len(outs), now - cur.t0)
+        self.timing["post"] += time.perf_counter() - now
+        return outs
+
+    def _account(self, batch, n_out: int, seconds: float):
+        self.total_steps += 1
+        self.total_generated += n_out
+        self.last_step = StepStats(len(batch.seqs), batch.num_tokens, batch.num_decode, seconds)
+        self.batch_size_history.append(len(batch.seqs))
+        if len(self.batch_size_history) > 4096:
+            del self.batch_size_history[:2048]
+
+    def _sync_step(self, batch, t0: float) -> list[RequestOutput]:
+        with self.lock:
             toks = self.runner.execute(batch)
             now = time.perf_counter()
-            self.timing["schedule"] += t0 - ts
             self.timing["execute"] += now - t0
             self.timing["steps"] += 1
             outs = []
@@ -133,29 +230,26 @@ class LLMEngine:
                 if reason:
                     self.scheduler.finish(seq, reason)
                 outs.append(self._output(seq, [tok]))
-            self.total_steps += 1
-            self.total_generated += len(outs)
-            self.last_step = StepStats(len(batch.seqs), batch.num_tokens, batch.num_decode,
-                                       now - t0)
-            self.batch_size_history.append(len(batch.seqs))
-            if len(self.batch_size_history) > 4096:
-                del self.batch_size_history[:2048]
+            self._account(batch, len(outs), now - t0)
             self.timing["post"] += time.perf_counter() - now
             return outs
 
-    def _stop_reason(self, seq: Sequence, tok: int) -> str | None:
+    def _stop_reason(self, seq: Sequence, tok: int, n_out: int | None = None) -> str | None:
+        """``n_out``: output tokens up to and including ``tok`` (default: all of them)."""
         sp = seq.sampling
+        n_out = len(seq.output_ids) if n_out is None else n_out
         if not sp.ignore_eos and (tok in self.eos_ids or tok in sp.stop_token_ids):
             return "stop"
-        if len(seq.output_ids) >= sp.max_tokens:
+        if n_out >= sp.max_tokens:
             return "length"
-        if seq.num_tokens >= self.cfg.max_model_len:
+        if seq.num_prompt + n_out >= self.cfg.max_model_len:
             return "length"
         return None
 
-    def _output(self, seq: Sequence, new) -> RequestOutput:
+    def _output(self, seq: Sequence, new, upto: int | None = None) -> RequestOutput:
+        ids = seq.output_ids if upto is None else seq.output_ids[:upto]
         return RequestOutput(
-            request_id=seq.request_id, token_ids=list(seq.output_ids), finished=seq.finished,
+            request_id=seq.request_id, token_ids=list(ids), finished=seq.finished,
             finish_reason=seq.finish_reason, prompt_tokens=seq.num_prompt,
             cached_prompt_tokens=seq.num_cached_prompt, arrival_time=seq.arrival_time,
             first_token_time=seq.first_token_time, first_scheduled_time=seq.first_scheduled_time,

@@ -63,6 +63,7 @@ class MetaLayout:
         add("seq_qstart", S + 1)
         add("tile_seq", NT)
         add("tile_qoff", NT)
+        add("feed_prev", 1)     # 1: decode rows take the previous step's device samples
         add("temperature", S, torch.float32)
         add("logits_idx", S, torch.int64)
         add("seeds", S, torch.int64)
@@ -147,9 +148,19 @@ class ModelRunner:
         self.max_layout = MetaLayout(self.max_tokens, self.max_seqs, self.bt_width,
                                      self.max_tokens)
         pin = self.is_cuda
-        self.meta_host = torch.zeros(self.max_layout.size, dtype=torch.int32, pin_memory=pin)
-        self.meta_host_np = self.meta_host.numpy()
+        # two pinned metadata buffers, used alternately: a step's H2D copy may still be queued
+        # while the host packs the next step (async look-ahead decode, TP workers); an event
+        # per buffer orders reuse behind the copy that last read it
+        self.meta_hosts = [torch.zeros(self.max_layout.size, dtype=torch.int32, pin_memory=pin)
+                           for _ in range(2)]
+        self.meta_hosts_np = [h.numpy() for h in self.meta_hosts]
+        self._mh = 0
+        self._h2d_done = [torch.cuda.Event() if self.is_cuda else None for _ in range(2)]
         self.meta_dev = torch.zeros(self.max_layout.size, dtype=torch.int32, device=self.device)
+        # sampled tokens of in-flight steps land here (D2H, one slot per in-flight step)
+        self.tok_host = [torch.zeros(max(cfg.max_num_seqs, 256), dtype=torch.int64,
+                                     pin_memory=pin) for _ in range(2)]
+        self._tok_done = [torch.cuda.Event() if self.is_cuda else None for _ in range(2)]
         nkv = self.model.n_kv_heads
         self.part_out = torch.empty(self.max_seqs * nkv * alloc_parts * 16 * 128,
                                     dtype=torch.float32, device=self.device)
@@ -249,11 +260,35 @@ class ModelRunner:
             seeds[i] = seq.seed
             steps[i] = len(seq.output_ids)
         arrays = dict(d)
-        arrays.update(input_ids=input_ids, temperature=temps, seeds=seeds, steps=steps)
+        arrays.update(input_ids=input_ids, temperature=temps, seeds=seeds, steps=steps,
+                      feed_prev=np.zeros(1, dtype=np.int32))
         return lay, arrays
 
+    @property
+    def meta_host(self) -> torch.Tensor:
+        return self.meta_hosts[self._mh]
+
+    @property
+    def meta_host_np(self) -> np.ndarray:
+        return self.meta_hosts_np[self._mh]
+
+    def _next_meta_host(self) -> np.ndarray:
+        """Switch to the other pinned metadata buffer (waiting for the H2D copy that last
+        read it) and return its numpy view."""
+        self._mh ^= 1
+        ev = self._h2d_done[self._mh]
+        if ev is not None:
+            ev.synchronize()
+        return self.meta_hosts_np[self._mh]
+
+    def _h2d(self, dst: torch.Tensor, size: int):
+        dst.copy_(self.meta_host[:size], non_blocking=True)
+        ev = self._h2d_done[self._mh]
+        if ev is not None:
+            ev.record()
+
     def _pack(self, lay: MetaLayout, arrays: dict) -> np.ndarray:
-        host = self.meta_host_np[:lay.size]
+        host = self._next_meta_host()[:lay.size]
         lay.pack(host, arrays)
         return host
 
@@ -270,9 +305,13 @@ class ModelRunner:
         if (self.fused_decode and special_sampling is None and md.num_tiles == 0
                 and md.num_decode == T and m.decode_fusable(T)):
             return m.forward_decode(v["input_ids"], md, self.k_layers, self.v_layers,
-                                    self._ws_for(T), v["temperature"], v["seeds"], v["steps"])
+                                    self._ws_for(T), v["temperature"], v["seeds"], v["steps"],
+                                    prev_tokens=self.ws["tokens"], feed_prev=v["feed_prev"])
+        decode_only = md.num_tiles == 0 and md.num_decode == T
         hidden = m.forward(v["input_ids"], md, self.k_layers, self.v_layers, self.part_out,
-                           self.part_lse, num_parts, self.part_tokens)
+                           self.part_lse, num_parts, self.part_tokens,
+                           prev_tokens=self.ws["tokens"] if decode_only else None,
+                           feed_prev=v["feed_prev"] if decode_only else None)
         last = hidden.index_select(0, v["logits_idx"])
         logits = m.compute_logits(last)
         if special_sampling is not None:
@@ -280,59 +319,117 @@ class ModelRunner:
         return ops.sample(logits, v["temperature"], v["seeds"], v["steps"])
 
     # ------------------------------------------------------------------------------------
+    def graph_bucket(self, batch: Batch) -> int:
+        """Graph bucket a decode-only batch replays from (0: eager step)."""
+        n = len(batch.seqs)
+        if not (self.is_cuda and self.cfg.use_graphs and batch.num_decode == n and n > 0
+                and self.graph_sizes and n <= self.graph_sizes[-1]):
+            return 0
+        if any(s.sampling.top_p < 1.0 or s.sampling.top_k > 0 for s in batch.seqs):
+            return 0
+        return next(b for b in self.graph_sizes if b >= n)
+
     def execute(self, batch: Batch) -> np.ndarray:
         """Run one step; returns sampled token ids (one per sequence in batch order)."""
         n = len(batch.seqs)
+        bucket = self.graph_bucket(batch)
+        if bucket:
+            return self.collect(self.launch(batch))
         self.steps += 1
         special = any(s.sampling.top_p < 1.0 or s.sampling.top_k > 0 for s in batch.seqs)
-        decode_only = batch.num_decode == n
-        bucket = 0
-        if (self.is_cuda and self.cfg.use_graphs and decode_only and not special
-                and self.graph_sizes and n <= self.graph_sizes[-1]):
-            bucket = next(b for b in self.graph_sizes if b >= n)
-            if bucket not in self.graphs:
-                self.capture(bucket)
+        lay, arrays = self._prepare(batch)
+        max_kv = int(arrays["seq_kvlen"][:batch.num_decode].max()) if batch.num_decode else 0
+        num_parts = max(1, math.ceil(max_kv / self.part_tokens))
+        host = self._pack(lay, arrays)
+        hdr = np.array([OP_STEP, lay.T, lay.S, lay.W, lay.NT, batch.num_decode, num_parts,
+                        0, int(special), n, lay.size, 0], dtype=np.int32)
+        if self.publisher is not None:
+            self.publisher.publish(np.concatenate([hdr, host]))
+        sampler = self._special_sampler(batch) if special else None
+        toks = self._run(hdr, sampler)
+        return toks[:n].cpu().numpy()
+
+    def launchable(self, batch: Batch) -> bool:
+        """Decode-only batches with plain sampling can be launched asynchronously."""
+        n = len(batch.seqs)
+        return (0 < n <= self.max_seqs and batch.num_decode == n
+                and not any(s.sampling.top_p < 1.0 or s.sampling.top_k > 0 for s in batch.seqs))
+
+    def launch(self, batch: Batch, lookahead: bool = False) -> dict:
+        """Enqueue one decode-only step (graph replay when a bucket fits, else eager) and its
+        token D2H copy; returns a handle for ``collect``.  ``lookahead``: the batch continues
+        the previous launch row for row and its input tokens are that step's device samples
+        (``ws["tokens"]``, not yet seen by the host), so the host never waits between steps
+        (async look-ahead decode)."""
+        if not self.launchable(batch):
+            raise ValueError("launch() needs a decode-only batch with plain sampling")
+        n = len(batch.seqs)
+        bucket = self.graph_bucket(batch)
+        if bucket and bucket not in self.graphs:
+            self.capture(bucket)
+        self.steps += 1
         t0 = time.perf_counter()
         if bucket:
             lay, arrays = self._prepare(batch, pad_seqs=bucket, tiles=False)
             assert lay.size == self.graph_io[bucket]["layout"].size
             num_parts = self.max_parts
         else:
-            lay, arrays = self._prepare(batch)
-            max_kv = int(arrays["seq_kvlen"][:batch.num_decode].max()) if batch.num_decode else 0
+            lay, arrays = self._prepare(batch, tiles=False)
+            max_kv = int(arrays["seq_kvlen"][:n].max())
             num_parts = max(1, math.ceil(max_kv / self.part_tokens))
+        arrays["feed_prev"] = np.array([1 if lookahead else 0], dtype=np.int32)
         host = self._pack(lay, arrays)
         hdr = np.array([OP_STEP, lay.T, lay.S, lay.W, lay.NT, batch.num_decode, num_parts,
-                        bucket, int(special), n, lay.size, 0], dtype=np.int32)
+                        bucket, 0, n, lay.size, 0], dtype=np.int32)
         if self.publisher is not None:
             self.publisher.publish(np.concatenate([hdr, host]))
-        sampler = self._special_sampler(batch) if special else None
         t1 = time.perf_counter()
-        toks = self._run(hdr, sampler)
-        out = toks[:n].cpu().numpy()
+        self._run(hdr)
+        dev_toks = self.ws["tokens"]  # _run leaves decode samples here (graph or eager)
+        slot = self._mh  # one token slot per metadata buffer: same reuse distance
+        ev = self._tok_done[slot]
+        if ev is not None:
+            ev.synchronize()
+        self.tok_host[slot][:n].copy_(dev_toks[:n], non_blocking=self.is_cuda)
+        if ev is not None:
+            ev.record()
         if bucket:
             self.timing["graph_prep"] += t1 - t0
-            self.timing["graph_run"] += time.perf_counter() - t1
-        return out
+        return {"n": n, "slot": slot, "t_launch": t1, "graph": bool(bucket)}
+
+    def collect(self, h: dict) -> np.ndarray:
+        """Wait for a launched step's tokens."""
+        ev = self._tok_done[h["slot"]]
+        if ev is not None:
+            ev.synchronize()
+        if h["graph"]:
+            self.timing["graph_run"] += time.perf_counter() - h["t_launch"]
+        return self.tok_host[h["slot"]][:h["n"]].numpy().copy()
 
     def _run(self, hdr, sampler=None, worker: bool = False):
         """Execute one step from its header; the packed metadata is in ``meta_host``."""
         T, S, W, NT, num_decode, num_parts, bucket, special, n, size = (int(x) for x in hdr[1:11])
         if bucket:
             io = self.graph_io[bucket]
-            io["dev"].copy_(self.meta_host[:size], non_blocking=True)
+            self._h2d(io["dev"], size)
             self.graphs[bucket].replay()
             self.graph_steps += 1
             return io["out"]
         lay = MetaLayout(T, S, W, NT)
         dev = self.meta_dev[:size]
-        dev.copy_(self.meta_host[:size], non_blocking=True)
+        self._h2d(dev, size)
         v = lay.views(dev)
         md = self._meta(v, num_decode, NT)
         if special and worker:
             # rank 0 samples (top-p / top-k); workers only join the logits all-gather
             sampler = _discard_sampler
-        return self._forward_sample(v, md, num_parts, sampler)
+        out = self._forward_sample(v, md, num_parts, sampler)
+        if not special and NT == 0 and num_decode == T and out is not None:
+            # every rank keeps the decode samples where a look-ahead step embeds them from
+            dev_toks = self.ws["tokens"]
+            if out.data_ptr() != dev_toks.data_ptr():
+                dev_toks[:T].copy_(out[:T])
+        return out
 
     # -- TP worker side ------------------------------------------------------------------
     def serve_worker(self, channel, reader: int) -> None:
@@ -366,12 +463,11 @@ class ModelRunner:
                 self.comm.barrier()
                 continue
             size = int(hdr[10])
-            self.meta_host_np[:size] = data[HDR_WORDS:HDR_WORDS + size]
+            # alternate pinned buffers: no stream sync per step, only an event wait on the
+            # copy two steps back before its buffer is rewritten
+            self._next_meta_host()[:size] = data[HDR_WORDS:HDR_WORDS + size]
             self._run(hdr, worker=True)
             self.steps += 1
-            if self.is_cuda:
-                # meta_host is reused by the next message: drain this step's H2D copy first
-                torch.cuda.current_stream(self.device).synchronize()
 
     def barrier(self):
         """Synchronise every TP rank (device work drained, then a process-group barrier)."""

@@ -362,19 +362,22 @@ class LlamaModel:
             if self.tp_size == 1:
                 ops.linear(a2, L.o_ps if ps else L.o, residual=residual,
                            waves=ops.decode_waves("o", ps, L.o_s is not None),
-                           preshuffled=ps, w_scale=L.o_s)
+                           preshuffled=ps, w_scale=L.o_s, ksplit=None, proj="o")
             else:
                 residual.add_(self._all_reduce(ops.linear(a2, L.o_ps if ps else L.o,
-                                                          preshuffled=ps, w_scale=L.o_s)))
+                                                          preshuffled=ps, w_scale=L.o_s,
+                                                          ksplit=None, proj="o")))
             ops.decode_gate_up_silu(residual, L.gate_up_ps if ps else L.gate_up, eps, out=act,
                                     preshuffled=ps, w_scale=L.gate_up_s)
             if self.tp_size == 1:
                 ops.linear(act, L.down_ps if ps else L.down, residual=residual,
                            waves=ops.decode_waves("down", ps, L.down_s is not None),
-                           preshuffled=ps, w_scale=L.down_s)
+                           preshuffled=ps, w_scale=L.down_s, ksplit=None,
+                           proj="down")
             else:
                 residual.add_(self._all_reduce(ops.linear(act, L.down_ps if ps else L.down,
-                                                          preshuffled=ps, w_scale=L.down_s)))
+                                                          preshuffled=ps, w_scale=L.down_s,
+                                                          ksplit=None, proj="down")))
         lm_ps = self.lm_head_ps is not None
         lm = self.lm_head_ps if lm_ps else self.lm_head
         if self.tp_size == 1:
@@ -388,7 +391,10 @@ class LlamaModel:
                                          vocab_offset=self.tp_rank * self.vocab_shard,
                                          preshuffled=lm_ps)
         self.tp_group.all_reduce_max(keys)
-        return ops.key_to_token(keys)
+        # tokens land in ws["tokens"] on every rank (an async look-ahead step embeds them)
+        toks = ws["tokens"][:B]
+        toks.copy_(ops.key_to_token(keys))
+        return toks
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
         logits = ops.linear(hidden, self.lm_head)

@@ -226,6 +226,55 @@ def decode_waves(proj: str, preshuffled: bool = False, fp8: bool = False) -> int
     return DECODE_WAVES[proj]["fp8" if fp8 else ("ps" if preshuffled else "rm")]
 
 
+# Split-K factor per decode projection: gridDim.y slices of K per 16-column tile so grids
+# that leave CUs idle (qkv: 384 tiles, o / down: 256 tiles on 256 CUs) stream from every CU;
+# the tile's last slice combines the fp32 partials in slice order (ops/csrc/gemv.hip).
+# 0 = auto (``auto_ksplit``).  The MI355X sweep (profiles/r2_microbench_splitk.txt) shows the
+# in-launch combine costs ~1.5-2 us, so splitting only pays when the grid is far below the
+# CU count: Llama-3.1-8B shapes (>= 256 tiles) all run fastest unsplit, the 70B TP=8 qkv
+# shard (80 tiles, K 8192) runs 14.7 -> 8.7 us at split 2.
+DECODE_KSPLIT = {"qkv": 0, "o": 0, "gate_up": 0, "down": 0}
+for _item in filter(None, os.environ.get("ATTA_DECODE_KSPLIT", "").split(",")):
+    _key, _, _val = _item.partition("=")
+    DECODE_KSPLIT[_key.strip()] = int(_val)
+
+
+def auto_ksplit(tiles: int, K: int) -> int:
+    """Split so a small grid reaches >= ~160 workgroups, keeping >= 2048 of K per slice."""
+    ks = 1
+    while tiles * ks < 160 and K // (ks * 2) >= 2048:
+        ks *= 2
+    return ks
+
+SPLITK_WS_FLOATS = 8 << 20   # 32 MiB: tiles x split x (32 x 16 + 32) fp32 slots
+SPLITK_COUNTERS = 8192
+_SPLITK_WS: dict = {}
+
+
+def ensure_splitk_workspace(device) -> None:
+    """Allocate + register the split-K workspace of ``device`` once (before any capture:
+    captured launches keep its address for the life of the graph)."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx in _SPLITK_WS:
+        return
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("split-K workspace must be allocated before hipGraph capture")
+    ws = torch.zeros(SPLITK_WS_FLOATS, dtype=torch.float32, device=f"cuda:{idx}")
+    counters = torch.zeros(SPLITK_COUNTERS, dtype=torch.int32, device=f"cuda:{idx}")
+    _native().set_splitk_workspace(ws, counters)
+    _SPLITK_WS[idx] = (ws, counters)
+
+
+def _ksplit(proj: str, x: torch.Tensor, ksplit: int | None, tiles: int) -> int:
+    k = DECODE_KSPLIT.get(proj, 0) if ksplit is None else ksplit
+    if k <= 0:
+        k = auto_ksplit(tiles, x.shape[1])
+    if k > 1:
+        ensure_splitk_workspace(x.device)
+    return k
+
+
 def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
     m, k = x.shape
     return (x.is_cuda and 1 <= m <= SKINNY_MAX_M and w.shape[0] % 16 == 0
@@ -331,7 +380,8 @@ def _need_cuda(x, preshuffled):
 
 def linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None,
            out: torch.Tensor | None = None, waves: int | None = None,
-           preshuffled: bool = False, w_scale: torch.Tensor | None = None) -> torch.Tensor:
+           preshuffled: bool = False, w_scale: torch.Tensor | None = None,
+           ksplit: int | None = 1, proj: str = "") -> torch.Tensor:
     """y = x @ w.T.  With ``residual`` the product is added to ``residual`` IN PLACE and
     ``residual`` is returned (residual-stream update).  Decode-sized M runs the MFMA skinny
     GEMM; everything else (prefill, CPU) runs F.linear (hipBLASLt on the GPU).
@@ -343,13 +393,15 @@ def linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = Non
     if preshuffled and not skinny_ok(x, w):
         raise ValueError("pre-shuffled weights need the skinny (decode) path")
     if skinny_ok(x, w):
+        ksplit = _ksplit(proj, x, ksplit, w.shape[0] // 16)
         if residual is not None:
             _native().skinny_gemm(residual, x, w, residual, waves or SKINNY_WAVES, preshuffled,
-                                  w_scale)
+                                  w_scale, ksplit)
             return residual
         if out is None:
             out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
-        _native().skinny_gemm(out, x, w, None, waves or SKINNY_WAVES, preshuffled, w_scale)
+        _native().skinny_gemm(out, x, w, None, waves or SKINNY_WAVES, preshuffled, w_scale,
+                              ksplit)
         return out
     y = torch.nn.functional.linear(x, w)
     if residual is not None:
@@ -363,7 +415,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = Non
 
 # ---- fused decode-step ops (norm weight folded into W on the host) -----------------------
 def decode_qkv_rope(x, w, eps, positions, slots, cos_sin, k_cache, v_cache, n_q_heads,
-                    n_kv_heads, q_out=None, preshuffled=False, w_scale=None):
+                    n_kv_heads, q_out=None, preshuffled=False, w_scale=None, ksplit=None):
     """RMSNorm(x) -> QKV GEMM -> RoPE -> q out + paged K/V write, one kernel on the GPU."""
     _need_cuda(x, preshuffled or w_scale is not None)
     if q_out is None:
@@ -377,11 +429,12 @@ def decode_qkv_rope(x, w, eps, positions, slots, cos_sin, k_cache, v_cache, n_q_
     _native().fused_qkv_rope(q_out, k_cache, v_cache, x, w, positions, slots, cos_sin,
                              n_q_heads, n_kv_heads, eps,
                              decode_waves("qkv", preshuffled, w_scale is not None),
-                             preshuffled or w_scale is not None, w_scale)
+                             preshuffled or w_scale is not None, w_scale,
+                             _ksplit("qkv", x, ksplit, w.shape[0] // 16))
     return q_out
 
 
-def decode_gate_up_silu(x, w, eps, out=None, preshuffled=False, w_scale=None):
+def decode_gate_up_silu(x, w, eps, out=None, preshuffled=False, w_scale=None, ksplit=None):
     """RMSNorm(x) -> gate_up GEMM -> SiLU(gate) * up, one kernel on the GPU."""
     _need_cuda(x, preshuffled or w_scale is not None)
     inter = w.shape[0] // 2
@@ -393,7 +446,7 @@ def decode_gate_up_silu(x, w, eps, out=None, preshuffled=False, w_scale=None):
         return out
     waves = decode_waves("gate_up", preshuffled, w_scale is not None)
     _native().fused_gate_up_silu(out, x, w, eps, waves, preshuffled or w_scale is not None,
-                                 w_scale)
+                                 w_scale, _ksplit("gate_up", x, ksplit, w.shape[0] // 16))
     return out
 
 

@@ -215,7 +215,7 @@ int skinny_dtype(const at::Tensor& x, bool preshuffled) {
 
 void skinny_gemm(at::Tensor y, const at::Tensor& x, const at::Tensor& w,
                  const c10::optional<at::Tensor>& residual, int64_t waves, bool preshuffled,
-                 const c10::optional<at::Tensor>& w_scale) {
+                 const c10::optional<at::Tensor>& w_scale, int64_t ksplit) {
   check_dev(x, "x");
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "skinny_gemm: 2-D operands");
   TORCH_CHECK(x.stride(1) == 1 && y.stride(1) == 1 && w.is_contiguous(), "skinny_gemm: layout");
@@ -234,7 +234,7 @@ void skinny_gemm(at::Tensor y, const at::Tensor& x, const at::Tensor& w,
   }
   const at::DeviceGuard g(x.device());
   check_rc(atta_skinny_gemm(y.data_ptr(), x.data_ptr(), w.data_ptr(), r, x.size(0), w.size(0),
-                            w.size(1), x.stride(0), y.stride(0), rs, waves, ws,
+                            w.size(1), x.stride(0), y.stride(0), rs, waves, ksplit, ws,
                             skinny_dtype(x, preshuffled), cur_stream()),
            "skinny_gemm");
 }
@@ -252,7 +252,8 @@ void check_skinny(const at::Tensor& x, const at::Tensor& w, const char* what) {
 void fused_qkv_rope(at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache, const at::Tensor& x,
                     const at::Tensor& w, const at::Tensor& positions, const at::Tensor& slots,
                     const at::Tensor& cos_sin, int64_t n_q_heads, int64_t n_kv_heads, double eps,
-                    int64_t waves, bool preshuffled, const c10::optional<at::Tensor>& w_scale) {
+                    int64_t waves, bool preshuffled, const c10::optional<at::Tensor>& w_scale,
+                    int64_t ksplit) {
   check_skinny(x, w, "fused_qkv_rope");
   const float* ws = fp8_scale(w, w_scale, "fused_qkv_rope");
   TORCH_CHECK(w.size(0) == (n_q_heads + 2 * n_kv_heads) * 128, "fused_qkv_rope: w rows");
@@ -266,14 +267,14 @@ void fused_qkv_rope(at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache, co
                                x.data_ptr(), w.data_ptr(), positions.data_ptr<int>(),
                                slots.data_ptr<int>(), cos_sin.data_ptr<float>(), x.size(0),
                                x.size(1), x.stride(0), q_out.stride(0), n_q_heads, n_kv_heads,
-                               k_cache.size(2), static_cast<float>(eps), waves, ws,
+                               k_cache.size(2), static_cast<float>(eps), waves, ksplit, ws,
                                skinny_dtype(x, preshuffled), cur_stream()),
            "fused_qkv_rope");
 }
 
 void fused_gate_up_silu(at::Tensor out, const at::Tensor& x, const at::Tensor& w, double eps,
                         int64_t waves, bool preshuffled,
-                        const c10::optional<at::Tensor>& w_scale) {
+                        const c10::optional<at::Tensor>& w_scale, int64_t ksplit) {
   check_skinny(x, w, "fused_gate_up_silu");
   const float* ws = fp8_scale(w, w_scale, "fused_gate_up_silu");
   TORCH_CHECK(w.size(0) == 2 * out.size(1) && out.size(0) == x.size(0) && out.stride(1) == 1,
@@ -281,7 +282,7 @@ void fused_gate_up_silu(at::Tensor out, const at::Tensor& x, const at::Tensor& w
   const at::DeviceGuard g(x.device());
   check_rc(atta_fused_gate_up_silu(out.data_ptr(), x.data_ptr(), w.data_ptr(), x.size(0),
                                    x.size(1), out.size(1), x.stride(0), out.stride(0),
-                                   static_cast<float>(eps), waves, ws,
+                                   static_cast<float>(eps), waves, ksplit, ws,
                                    skinny_dtype(x, preshuffled), cur_stream()),
            "fused_gate_up_silu");
 }
@@ -309,6 +310,21 @@ void fused_lm_head_sample(at::Tensor tokens, at::Tensor keys, const at::Tensor& 
                static_cast<int>(finalize), static_cast<int>(vocab_offset), waves, ws,
                skinny_dtype(x, preshuffled), cur_stream()),
            "fused_lm_head_sample");
+}
+
+// Registers the split-K workspace of the skinny GEMVs on ws's device.  The tensors must
+// outlive every launch (and captured graph) that uses a split > 1; counters start zeroed.
+void set_splitk_workspace(const at::Tensor& ws, const at::Tensor& counters) {
+  check_dev(ws, "ws");
+  check_dev(counters, "counters");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() &&
+                  counters.scalar_type() == at::kInt && counters.is_contiguous() &&
+                  ws.device() == counters.device(),
+              "set_splitk_workspace: fp32 ws + int32 counters on one device");
+  TORCH_CHECK(ws.numel() < (int64_t(1) << 29), "set_splitk_workspace: ws must stay under 2 GiB");
+  check_rc(atta_set_splitk_ws(ws.device().index(), ws.data_ptr<float>(), counters.data_ptr<int>(),
+                              ws.numel(), static_cast<int>(counters.numel())),
+           "set_splitk_workspace");
 }
 
 void sample_finalize(at::Tensor tokens, const at::Tensor& keys, int64_t n_tiles) {
@@ -434,16 +450,17 @@ TORCH_LIBRARY(atta, m) {
   m.def(
       "fused_qkv_rope(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor x, "
       "Tensor w, Tensor positions, Tensor slots, Tensor cos_sin, int n_q_heads, int n_kv_heads, "
-      "float eps, int waves, bool preshuffled=False, Tensor? w_scale=None) -> ()");
+      "float eps, int waves, bool preshuffled=False, Tensor? w_scale=None, int ksplit=1) -> ()");
   m.def("fused_gate_up_silu(Tensor(a!) out, Tensor x, Tensor w, float eps, int waves, "
-        "bool preshuffled=False, Tensor? w_scale=None) -> ()");
+        "bool preshuffled=False, Tensor? w_scale=None, int ksplit=1) -> ()");
+  m.def("set_splitk_workspace(Tensor ws, Tensor counters) -> ()");
   m.def(
       "fused_lm_head_sample(Tensor(a!) tokens, Tensor(b!) keys, Tensor x, Tensor w, float eps, "
       "Tensor temperature, Tensor seeds, Tensor steps, int finalize, int vocab_offset, "
       "int waves, bool preshuffled=False, Tensor? w_scale=None) -> ()");
   m.def("sample_finalize(Tensor(a!) tokens, Tensor keys, int n_tiles) -> ()");
   m.def("skinny_gemm(Tensor(a!) y, Tensor x, Tensor w, Tensor? residual, int waves, "
-        "bool preshuffled=False, Tensor? w_scale=None) -> ()");
+        "bool preshuffled=False, Tensor? w_scale=None, int ksplit=1) -> ()");
   m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rms_norm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
@@ -479,6 +496,7 @@ TORCH_LIBRARY_IMPL(atta, CUDA, m) {
   m.impl("fused_gate_up_silu", &fused_gate_up_silu);
   m.impl("fused_lm_head_sample", &fused_lm_head_sample);
   m.impl("sample_finalize", &sample_finalize);
+  m.impl("set_splitk_workspace", &set_splitk_workspace);
   m.impl("attention_decode_v2", &attention_decode_v2);
   m.impl("skinny_variant", &skinny_variant);
 }

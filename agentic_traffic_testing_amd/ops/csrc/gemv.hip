@@ -99,6 +99,12 @@ struct SkinnyParams {
   const float* temperature;
   const int64_t* seeds;
   const int64_t* steps;
+  // split-K (gridDim.y = ksplit slices of K per 16-column tile): each slice publishes its
+  // fp32 partial tile (+ row sum-of-squares) to sk_ws; the tile's last arriving slice sums
+  // them in slice order (bitwise deterministic) and runs the epilogue
+  int ksplit;
+  float* sk_ws;
+  int* sk_counters;
 };
 
 __device__ __forceinline__ unsigned ordered_bits(float f) {
@@ -146,14 +152,17 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
   __shared__ float red[WAVES][R][17];
   __shared__ float ssq[WAVES][R];
   __shared__ float inv_rms[R];
+  __shared__ int sk_last;
 
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int col = lane & 15;
   const int grp = lane >> 4;
   const int tile = blockIdx.x;
-  const int kw = p.K / WAVES;
-  const int kbeg = wid * kw;
+  const int ks = blockIdx.y;  // split-K slice
+  const int kslice = p.K / p.ksplit;
+  const int kw = kslice / WAVES;
+  const int kbeg = ks * kslice + wid * kw;
   const int wrow = tile_row<EPI>(tile, col, p);
   const uint16_t* wp =
       PS ? p.w + (static_cast<int64_t>(tile) * (p.K / 32) + kbeg / 32) * 512 + lane * 8
@@ -270,11 +279,12 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
     }
   }
   __syncthreads();
+  // inv_rms[] holds the row sum of squares until the rsqrt below
   if (norm && threadIdx.x < R) {
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < WAVES; ++q) s += ssq[q][threadIdx.x];
-    inv_rms[threadIdx.x] = rsqrtf(s / static_cast<float>(p.K) + p.eps);
+    inv_rms[threadIdx.x] = s;
   }
   // sum wave partials into red[0] (fp8 weights: times the row's dequant scale)
   for (int e = threadIdx.x; e < R * 16; e += WAVES * 64) {
@@ -285,6 +295,45 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
     if constexpr (W8) s *= p.wscale[tile_row<EPI>(tile, n, p)];
     red[0][m][n] = s;
   }
+  __syncthreads();
+  if (p.ksplit > 1) {
+    // ---- split-K hand-over (device-scope sc1 stores/loads + arrival counter, no fences:
+    // common.h "device-coherent hand-over"); slot = R*16 partial sums + R row sums of squares
+    constexpr int kSlot = R * 16 + R;
+    const auto rws = dev_rsrc(p.sk_ws);
+    const uint32_t mine = static_cast<uint32_t>((tile * p.ksplit + ks) * kSlot) * 4u;
+    for (int e = threadIdx.x; e < R * 16; e += WAVES * 64)
+      if ((e >> 4) < p.M) dev_store4(rws, mine + e * 4, red[0][e >> 4][e & 15]);
+    if (norm && threadIdx.x < R && threadIdx.x < p.M)
+      dev_store4(rws, mine + (R * 16 + threadIdx.x) * 4, inv_rms[threadIdx.x]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores acknowledged
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int old = __hip_atomic_fetch_add(p.sk_counters + tile, 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      sk_last = (old == p.ksplit - 1);
+    }
+    __syncthreads();
+    if (!sk_last) return;  // block-uniform
+    const uint32_t first = static_cast<uint32_t>(tile * p.ksplit * kSlot) * 4u;
+    for (int e = threadIdx.x; e < R * 16; e += WAVES * 64) {
+      if ((e >> 4) >= p.M) continue;
+      float s = 0.f;
+      for (int q = 0; q < p.ksplit; ++q) s += dev_load4(rws, first + (q * kSlot + e) * 4);
+      red[0][e >> 4][e & 15] = s;
+    }
+    if (norm && threadIdx.x < R && threadIdx.x < p.M) {
+      float s = 0.f;
+      for (int q = 0; q < p.ksplit; ++q)
+        s += dev_load4(rws, first + (q * kSlot + R * 16 + threadIdx.x) * 4);
+      inv_rms[threadIdx.x] = s;
+    }
+    if (threadIdx.x == 0)
+      __hip_atomic_store(p.sk_counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+  }
+  if (norm && threadIdx.x < R)
+    inv_rms[threadIdx.x] = rsqrtf(inv_rms[threadIdx.x] / static_cast<float>(p.K) + p.eps);
   __syncthreads();
 
   // ---- epilogues -----------------------------------------------------------------------
@@ -508,17 +557,54 @@ static int skinny_checks(int M, int K, int waves) {
   return 0;
 }
 
+// Split-K workspace per device (ops.set_splitk_workspace): fp32 partial slots + one arrival
+// counter per 16-column tile (zeroed once; the last arriver re-arms it).
+struct SplitKWs {
+  float* ws = nullptr;
+  int* counters = nullptr;
+  int64_t ws_floats = 0;
+  int n_counters = 0;
+};
+static SplitKWs g_splitk[64];
+
+int atta_set_splitk_ws(int device, float* ws, int* counters, int64_t ws_floats, int n_counters) {
+  if (device < 0 || device >= 64) return -1;
+  g_splitk[device] = SplitKWs{ws, counters, ws_floats, n_counters};
+  return 0;
+}
+
+// Resolve the split for one launch: waves fitted to the K slice (fp8: 64-wide granule), the
+// split reduced until every wave's slice is whole; a split > 1 needs the device workspace.
+// Returns 0 or -1 (unsupported), -2 (split requested but no / too small workspace).
+static int setup_split(SkinnyParams& p, int& waves, int ksplit, int tiles, bool fp8) {
+  const int gran = fp8 ? 64 : 32;
+  if (ksplit < 1) ksplit = 1;
+  while (ksplit > 1 && p.K % (ksplit * gran * 4) != 0) ksplit >>= 1;
+  waves = fit_waves(waves, p.K / ksplit, fp8);
+  if ((p.K / ksplit) % (gran * waves) != 0) return -1;
+  p.ksplit = ksplit;
+  if (ksplit == 1) return 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -2;
+  const SplitKWs& w = g_splitk[dev];
+  const int64_t slot = static_cast<int64_t>(p.M <= 16 ? 16 : 32) * 17;
+  if (w.ws == nullptr || tiles > w.n_counters ||
+      static_cast<int64_t>(tiles) * ksplit * slot > w.ws_floats)
+    return -2;
+  p.sk_ws = w.ws;
+  p.sk_counters = w.counters;
+  return 0;
+}
+
 int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual, int M, int N,
                      int K, int64_t x_stride, int64_t y_stride, int64_t res_stride, int waves,
-                     const float* wscale, int dtype, hipStream_t stream) {
+                     int ksplit, const float* wscale, int dtype, hipStream_t stream) {
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
-  waves = fit_waves(waves, K, wscale != nullptr);
-  if (skinny_checks(M, K, waves) || N % 16 != 0) return -1;
+  if (M < 1 || M > 32 || N % 16 != 0) return -1;
   SkinnyParams p{};
   p.ps = ps;
   p.wscale = wscale;
-  if (wscale != nullptr && (K / waves) % 64 != 0) return -1;
   p.x = static_cast<const uint16_t*>(x);
   p.w = static_cast<const uint16_t*>(w);
   p.M = M;
@@ -526,8 +612,9 @@ int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual
   p.K = K;
   p.x_stride = x_stride;
   p.eps = 0.f;
+  if (const int rc = setup_split(p, waves, ksplit, N / 16, wscale != nullptr)) return rc;
   const int mt = M <= 16 ? 1 : 2;
-  dim3 grid(N / 16);
+  dim3 grid(N / 16, p.ksplit);
   if (residual != nullptr) {
     // y := residual + x W^T, computed in place on the residual buffer when y == residual;
     // otherwise copy semantics are not supported (callers pass y == residual).
@@ -546,18 +633,17 @@ int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual
 int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x, const void* w,
                         const int* positions, const int* slots, const float* cos_sin, int M,
                         int K, int64_t x_stride, int64_t q_stride, int n_q_heads, int n_kv_heads,
-                        int block_size, float eps, int waves, const float* wscale, int dtype, hipStream_t stream) {
+                        int block_size, float eps, int waves, int ksplit, const float* wscale,
+                        int dtype, hipStream_t stream) {
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
-  waves = fit_waves(waves, K, wscale != nullptr);
-  if (skinny_checks(M, K, waves)) return -1;
+  if (M < 1 || M > 32) return -1;
   int shift = 0;
   while ((1 << shift) < block_size) ++shift;
   if ((1 << shift) != block_size) return -1;
   SkinnyParams p{};
   p.ps = ps;
   p.wscale = wscale;
-  if (wscale != nullptr && (K / waves) % 64 != 0) return -1;
   p.x = static_cast<const uint16_t*>(x);
   p.w = static_cast<const uint16_t*>(w);
   p.y = static_cast<uint16_t*>(q_out);
@@ -575,22 +661,21 @@ int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x
   p.n_q_heads = n_q_heads;
   p.n_kv_heads = n_kv_heads;
   p.bs_shift = shift;
-  dim3 grid(p.N / 16);
+  if (const int rc = setup_split(p, waves, ksplit, p.N / 16, wscale != nullptr)) return rc;
+  dim3 grid(p.N / 16, p.ksplit);
   launch_epi<EPI_QKVROPE>(dtype, M <= 16 ? 1 : 2, waves, grid, stream, p);
   return static_cast<int>(hipGetLastError());
 }
 
 int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int K, int inter,
-                            int64_t x_stride, int64_t out_stride, float eps, int waves, const float* wscale, int dtype,
-                            hipStream_t stream) {
+                            int64_t x_stride, int64_t out_stride, float eps, int waves,
+                            int ksplit, const float* wscale, int dtype, hipStream_t stream) {
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
-  waves = fit_waves(waves, K, wscale != nullptr);
-  if (skinny_checks(M, K, waves) || inter % 8 != 0) return -1;
+  if (M < 1 || M > 32 || inter % 8 != 0) return -1;
   SkinnyParams p{};
   p.ps = ps;
   p.wscale = wscale;
-  if (wscale != nullptr && (K / waves) % 64 != 0) return -1;
   p.x = static_cast<const uint16_t*>(x);
   p.w = static_cast<const uint16_t*>(w);
   p.y = static_cast<uint16_t*>(out);
@@ -601,7 +686,8 @@ int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int 
   p.N = 2 * inter;
   p.inter = inter;
   p.eps = eps;
-  dim3 grid(inter / 8);
+  if (const int rc = setup_split(p, waves, ksplit, inter / 8, wscale != nullptr)) return rc;
+  dim3 grid(inter / 8, p.ksplit);
   launch_epi<EPI_SILU>(dtype, M <= 16 ? 1 : 2, waves, grid, stream, p);
   return static_cast<int>(hipGetLastError());
 }
@@ -629,6 +715,7 @@ int atta_fused_lm_head_sample(int64_t* tokens, unsigned long long* keys, const v
   p.keys = keys;
   p.key_stride = N / 16;
   p.vocab_offset = vocab_offset;
+  p.ksplit = 1;
   p.temperature = temperature;
   p.seeds = seeds;
   p.steps = steps;
@@ -653,6 +740,7 @@ int atta_skinny_variant(void* y, const void* x, const void* w, int M, int N, int
   p.M = M;
   p.N = N;
   p.K = K;
+  p.ksplit = 1;
   if (M < 1 || M > 16 || N % 16) return -1;
   dim3 grid(N / 16);
   static const int waves_of[14] = {8, 8, 4, 4, 8, 16, 8, 16, 8, 16, 8, 16, 4, 4};

@@ -45,16 +45,20 @@ int atta_sample(int64_t* out, const void* logits, int rows, int vocab, int64_t s
 
 int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual, int M, int N,
                      int K, int64_t x_stride, int64_t y_stride, int64_t res_stride, int waves,
-                     const float* wscale, int dtype, hipStream_t stream);
+                     int ksplit, const float* wscale, int dtype, hipStream_t stream);
 
 int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x, const void* w,
                         const int* positions, const int* slots, const float* cos_sin, int M,
                         int K, int64_t x_stride, int64_t q_stride, int n_q_heads, int n_kv_heads,
-                        int block_size, float eps, int waves, const float* wscale, int dtype, hipStream_t stream);
+                        int block_size, float eps, int waves, int ksplit, const float* wscale,
+                        int dtype, hipStream_t stream);
 
 int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int K, int inter,
-                            int64_t x_stride, int64_t out_stride, float eps, int waves, const float* wscale, int dtype,
-                            hipStream_t stream);
+                            int64_t x_stride, int64_t out_stride, float eps, int waves,
+                            int ksplit, const float* wscale, int dtype, hipStream_t stream);
+
+// Split-K workspace of `device` for the skinny GEMVs (fp32 slots + per-tile counters, zeroed).
+int atta_set_splitk_ws(int device, float* ws, int* counters, int64_t ws_floats, int n_counters);
 
 int atta_fused_lm_head_sample(int64_t* tokens, unsigned long long* keys, const void* x,
                               const void* w, int M, int N, int K, int64_t x_stride, float eps,

@@ -107,3 +107,53 @@ def test_fp8_engine_gpu():
         if graphs:
             assert eng.runner.graph_steps > 0
     assert res[0] == res[1]
+
+
+def _gen(cfg_kw, prompts, sp):
+    eng = LLMEngine(EngineConfig(**cfg_kw))
+    outs = eng.generate(prompts, sp)
+    return eng, [(o.token_ids, o.finish_reason) for o in outs]
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_async_lookahead_decode_matches_sync(device):
+    """Async look-ahead decode (next step launched before the host sees the current step's
+    tokens; inputs fed on the device) produces exactly the synchronous engine's outputs:
+    sampled and greedy rows, different lengths, a stop token hit mid-flight (its look-ahead
+    token discarded) and a mid-run admission that drains the pipeline."""
+    kw = dict(model="tiny" if device == "cpu" else "small", device=device, max_model_len=256,
+              num_kv_blocks=128, max_num_batched_tokens=128, max_num_seqs=4,
+              use_graphs=device == "cuda", graph_batch_sizes=(1, 2, 4))
+    prompts = _prompts(vocab=3000)[:4]
+    greedy = SamplingParams(temperature=0.0, max_tokens=14, ignore_eos=True)
+    _, base = _gen(dict(kw, async_decode=False), prompts[:1], [greedy])
+    stop_tok = base[0][0][5]  # stops the greedy row at its 6th token (or earlier repeat)
+    sp = [SamplingParams(temperature=0.7, max_tokens=17, ignore_eos=True, seed=11),
+          SamplingParams(temperature=0.0, max_tokens=14, stop_token_ids=(stop_tok,)),
+          SamplingParams(temperature=0.5, max_tokens=9, ignore_eos=True, seed=5),
+          SamplingParams(temperature=0.2, max_tokens=21, ignore_eos=True, seed=2)]
+    order = [prompts[1], prompts[0], prompts[2], prompts[3]]
+    res = {}
+    for a in (False, True):
+        eng, res[a] = _gen(dict(kw, async_decode=a), order, sp)
+        if a:
+            assert eng.timing["lookahead_steps"] > 10
+            info = eng.kv_cache_info()
+            assert info["free_blocks"] == info["num_gpu_blocks"]
+    assert res[False] == res[True]
+    assert res[True][1][1] == "stop" and res[True][1][0][-1] == stop_tok
+    # staggered arrival: a request admitted while look-ahead steps are in flight
+    for a in (False, True):
+        eng = LLMEngine(EngineConfig(**dict(kw, async_decode=a)))
+        eng.add_request("r0", prompts[0], sp[0])
+        got = {}
+        steps = 0
+        while eng.has_unfinished():
+            for o in eng.step():
+                if o.finished:
+                    got[o.request_id] = o.token_ids
+            steps += 1
+            if steps == 5:
+                eng.add_request("r1", prompts[2], sp[3])
+        res[("stagger", a)] = got
+    assert res[("stagger", False)] == res[("stagger", True)]

@@ -243,6 +243,59 @@ def test_skinny_gemm(dtype, m, n, k):
     close(got_r, exp_r, 3e-2 * math.sqrt(k / 4096), 1e-2)
 
 
+@pytest.mark.parametrize("ksplit", [2, 4])
+@pytest.mark.parametrize("m,n,k", [(1, 1280, 8192), (5, 4096, 4096), (20, 2048, 14336)])
+def test_skinny_gemm_splitk(ksplit, m, n, k):
+    """Split-K GEMV (in-launch combine of fp32 slice partials by the last arriving slice)
+    vs the fp32 reference, plain and residual epilogues, repeated so counters must re-arm."""
+    torch.manual_seed(17)
+    dt = torch.bfloat16
+    x = torch.randn(m, k, dtype=dt, device="cuda")
+    w = torch.randn(n, k, dtype=dt, device="cuda") * 0.02
+    wp = ops.preshuffle(w)
+    exp = x.float() @ w.float().t()
+    for _ in range(3):
+        got = ops.linear(x, wp, waves=4, preshuffled=True, ksplit=ksplit)
+        close(got, exp, 2e-2 * math.sqrt(k / 4096), 1e-2)
+        r = torch.randn(m, n, dtype=dt, device="cuda")
+        exp_r = exp.to(dt).float() + r.float()
+        ops.linear(x, wp, residual=r, waves=8, preshuffled=True, ksplit=ksplit)
+        close(r, exp_r, 3e-2 * math.sqrt(k / 4096), 1e-2)
+    ws, counters = ops._SPLITK_WS[torch.cuda.current_device()]
+    assert bool((counters == 0).all())
+    # slice partials are summed in slice order: the result is run-to-run bit-identical
+    a = ops.linear(x, wp, waves=4, preshuffled=True, ksplit=ksplit)
+    b = ops.linear(x, wp, waves=4, preshuffled=True, ksplit=ksplit)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("ksplit", [2, 4])
+def test_fused_decode_kernels_splitk(ksplit):
+    """Fused qkv+RoPE and gate_up+SiLU epilogues (RMSNorm row sums combined across slices)."""
+    torch.manual_seed(19)
+    dt, H, bs, nb, hq, hkv, m = torch.bfloat16, 8192, 16, 64, 8, 1, 5
+    x = torch.randn(m, H, dtype=dt, device="cuda") * 2
+    w = torch.randn((hq + 2 * hkv) * 128, H, dtype=dt, device="cuda") * 0.02
+    pos = torch.randint(0, 4000, (m,), dtype=torch.int32, device="cuda")
+    slots = torch.randperm(nb * bs, device="cuda")[:m].to(torch.int32)
+    cs = ref.rope_cos_sin(128, 8192, 500000.0, None, device="cuda")
+    k1, v1 = _rand_cache(nb, hkv, bs, 128, dt)
+    k2, v2 = k1.clone(), v1.clone()
+    q_exp = ref.rope_cache(torch.nn.functional.linear(_norm_ref(x), w), pos, slots, cs, k1, v1,
+                           hq, hkv, 128)
+    q_got = ops.decode_qkv_rope(x, ops.preshuffle(w, "qkv"), 1e-5, pos, slots, cs, k2, v2, hq,
+                                hkv, preshuffled=True, ksplit=ksplit)
+    close(q_got, q_exp, 3e-2, 2e-2)
+    close(k2, k1, 3e-2, 2e-2)
+    close(v2, v1, 3e-2, 2e-2)
+    inter = 1024
+    wg = torch.randn(2 * inter, H, dtype=dt, device="cuda") * 0.02
+    exp = ref.silu_and_mul(torch.nn.functional.linear(_norm_ref(x), wg))
+    got = ops.decode_gate_up_silu(x, ops.preshuffle(wg, "silu"), 1e-5, preshuffled=True,
+                                  ksplit=ksplit)
+    close(got, exp, 4e-2, 4e-2)
+
+
 def _norm_ref(x, eps=1e-5):
     return ref.rms_norm(x, torch.ones(x.shape[1], dtype=x.dtype, device=x.device), eps)
 
