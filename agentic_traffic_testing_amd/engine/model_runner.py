@@ -134,7 +134,7 @@ class ModelRunner:
         if self.max_parts_small > 64:  # in-kernel combine handles <= 64 partitions
             self.part_tokens_small, self.max_parts_small = self.part_tokens, self.max_parts
         alloc_parts = max(self.max_parts, self.max_parts_small)
-        self.tile_tokens = ops.PREFILL_TILE_TOKENS.get(self.model.g, 16)
+        self.tile_tokens = ops.prefill_tile_tokens(self.model.g)
         self.graph_sizes = sorted(b for b in cfg.graph_batch_sizes)
         if comm is not None and comm.size > 1 and comm.is_gloo:
             self.graph_sizes = []  # gloo collectives are host-side: nothing to capture

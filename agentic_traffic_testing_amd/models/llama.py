@@ -295,16 +295,14 @@ class LlamaModel:
         """Returns the final normed hidden state rows [T, H]."""
         cfg = self.cfg
         eps = cfg.rms_norm_eps
-        h = ops.embed(self.embed, input_ids, prev_tokens, feed_prev)
-        T = h.shape[0]
-        residual = torch.empty_like(h)
+        # the residual stream IS the embedding output: every row-parallel projection adds its
+        # product into it inside the GEMM epilogue (hipBLASLt beta=1 C-matrix epilogue, or the
+        # skinny GEMV's RESADD) - no separate add / copy passes over [T, hidden]
+        residual = ops.embed(self.embed, input_ids, prev_tokens, feed_prev)
+        T = residual.shape[0]
         nq, nkv, D = self.n_heads, self.n_kv_heads, self.head_dim
         for li, L in enumerate(self.layers):
-            if li == 0:
-                residual.copy_(h)
-                x = ops.rms_norm(h, L.input_norm, eps)
-            else:
-                x = ops.fused_add_rms_norm(h, residual, L.input_norm, eps)
+            x = ops.rms_norm(residual, L.input_norm, eps)
             qkv = self._proj(x, L.qkv, L.qkv_s)
             q = ops.rope_cache(qkv, md.positions, md.slot_mapping, self.cos_sin, k_caches[li],
                                v_caches[li], nq, nkv, D)
@@ -317,12 +315,19 @@ class LlamaModel:
                 ops.attention_prefill(q, k_caches[li], v_caches[li], md.block_tables,
                                       md.seq_kvlen, md.seq_qstart, md.tile_seq, md.tile_qoff,
                                       self.scale, out=attn)
-            h = self._all_reduce(self._proj(attn.view(T, nq * D), L.o, L.o_s))
-            x = ops.fused_add_rms_norm(h, residual, L.post_norm, eps)
+            self._proj_residual(attn.view(T, nq * D), L.o, L.o_s, residual)
+            x = ops.rms_norm(residual, L.post_norm, eps)
             gu = self._proj(x, L.gate_up, L.gate_up_s)
             a = ops.silu_and_mul(gu)
-            h = self._all_reduce(self._proj(a, L.down, L.down_s))
-        return ops.fused_add_rms_norm(h, residual, self.norm, eps)
+            self._proj_residual(a, L.down, L.down_s, residual)
+        return ops.rms_norm(residual, self.norm, eps)
+
+    def _proj_residual(self, x, w, scale, residual):
+        """residual += x @ w.T (row-parallel projection; TP: all-reduced partial sums)."""
+        if self.tp_size > 1:
+            residual.add_(self._all_reduce(self._proj(x, w, scale)))
+            return residual
+        return self._proj(x, w, scale, residual=residual)
 
     def decode_fusable(self, num_tokens: int) -> bool:
         # 16-bit GEMVs: K % 128 (4 waves x 32); fp8 GEMVs: K % 256 (4 waves x 64)

@@ -156,14 +156,31 @@ def rope_cache(qkv, positions, slot_mapping, cos_sin, k_cache, v_cache, n_q_head
     return q_out
 
 
+# Prefill attention kernel: "flash" = LDS-staged 32x32x16-MFMA flash kernel
+# (flash_prefill.hip, tiles of 128 / G tokens); "v1" = the round-1 per-wave kernel
+# (attention.hip, tiles of 64 / G ... 8 tokens; kept for A/B runs).
+PREFILL_IMPL = os.environ.get("ATTA_PREFILL_IMPL", "flash")
+
+
+def prefill_tile_tokens(g: int, impl: str | None = None) -> int:
+    """Query tokens per prefill attention workgroup for GQA group ``g``."""
+    if (impl or PREFILL_IMPL) == "flash":
+        return 128 // g
+    return PREFILL_TILE_TOKENS.get(g, 16)
+
+
 def attention_prefill(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, tile_seq,
-                      tile_qoff, scale, out=None):
+                      tile_qoff, scale, out=None, impl: str | None = None):
+    """Causal varlen prefill attention over the paged cache.  ``tile_seq`` / ``tile_qoff``
+    must come from tiles of ``prefill_tile_tokens(G, impl)`` tokens."""
     if not q.is_cuda:
         return ref.paged_attention(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart,
                                    scale, out=out)
     out = torch.empty_like(q) if out is None else out
-    _native().attention_prefill(out, q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart,
-                                tile_seq, tile_qoff, q.shape[1], k_cache.shape[1], scale)
+    fn = _native().flash_prefill if (impl or PREFILL_IMPL) == "flash" else \
+        _native().attention_prefill
+    fn(out, q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, tile_seq, tile_qoff,
+       q.shape[1], k_cache.shape[1], scale)
     return out
 
 
@@ -403,10 +420,15 @@ def linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = Non
         _native().skinny_gemm(out, x, w, None, waves or SKINNY_WAVES, preshuffled, w_scale,
                               ksplit)
         return out
-    y = torch.nn.functional.linear(x, w)
     if residual is not None:
-        residual.copy_((y.float() + residual.float()).to(residual.dtype))
+        # hipBLASLt C-matrix epilogue: residual = residual + x @ w.T in one GEMM (fp32
+        # accumulate, one rounding), no separate add pass over the residual stream
+        if residual.is_cuda:
+            return residual.addmm_(x, w.t())
+        residual.copy_((torch.nn.functional.linear(x, w).float() + residual.float())
+                       .to(residual.dtype))
         return residual
+    y = torch.nn.functional.linear(x, w)
     if out is not None:
         out.copy_(y)
         return out

@@ -148,6 +148,36 @@ void attention_prefill(at::Tensor out, const at::Tensor& q, const at::Tensor& k_
            "attention_prefill");
 }
 
+// LDS-staged flash prefill (flash_prefill.hip); tiles must hold 128 / G query tokens.
+void flash_prefill(at::Tensor out, const at::Tensor& q, const at::Tensor& k_cache,
+                   const at::Tensor& v_cache, const at::Tensor& block_tables,
+                   const at::Tensor& seq_kvlen, const at::Tensor& seq_qstart,
+                   const at::Tensor& tile_seq, const at::Tensor& tile_qoff, int64_t n_q_heads,
+                   int64_t n_kv_heads, double scale) {
+  check_dev(q, "q");
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && seq_kvlen.scalar_type() == at::kInt &&
+                  seq_qstart.scalar_type() == at::kInt && tile_seq.scalar_type() == at::kInt &&
+                  tile_qoff.scalar_type() == at::kInt,
+              "flash_prefill: metadata must be int32");
+  TORCH_CHECK(q.stride(-1) == 1 && out.stride(-1) == 1, "flash_prefill: last dim contiguous");
+  TORCH_CHECK(q.scalar_type() == out.scalar_type() && k_cache.scalar_type() == q.scalar_type() &&
+                  v_cache.scalar_type() == q.scalar_type(),
+              "flash_prefill: dtypes");
+  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 4 && k_cache.size(1) == n_kv_heads &&
+                  k_cache.size(3) == 128 && v_cache.size(2) == 128 &&
+                  v_cache.size(3) == k_cache.size(2),
+              "flash_prefill: caches [nb, Hkv, BS, 128] / [nb, Hkv, 128, BS]");
+  TORCH_CHECK(tile_qoff.numel() >= tile_seq.numel(), "flash_prefill: tile arrays");
+  const at::DeviceGuard g(q.device());
+  check_rc(atta_flash_prefill(
+               out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+               block_tables.data_ptr<int>(), seq_kvlen.data_ptr<int>(), seq_qstart.data_ptr<int>(),
+               tile_seq.data_ptr<int>(), tile_qoff.data_ptr<int>(), tile_seq.size(0), n_q_heads,
+               n_kv_heads, k_cache.size(3), k_cache.size(2), block_tables.stride(0), q.stride(0),
+               out.stride(0), static_cast<float>(scale), dtype_code(q), cur_stream()),
+           "flash_prefill");
+}
+
 void attention_decode(at::Tensor out, at::Tensor part_out, at::Tensor part_lse,
                       const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                       const at::Tensor& block_tables, const at::Tensor& seq_kvlen,
@@ -474,6 +504,10 @@ TORCH_LIBRARY(atta, m) {
       "Tensor block_tables, Tensor seq_kvlen, Tensor seq_qstart, Tensor tile_seq, "
       "Tensor tile_qoff, int n_q_heads, int n_kv_heads, float scale) -> ()");
   m.def(
+      "flash_prefill(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
+      "Tensor block_tables, Tensor seq_kvlen, Tensor seq_qstart, Tensor tile_seq, "
+      "Tensor tile_qoff, int n_q_heads, int n_kv_heads, float scale) -> ()");
+  m.def(
       "attention_decode(Tensor(a!) out, Tensor(b!) part_out, Tensor(c!) part_lse, Tensor q, "
       "Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor seq_kvlen, "
       "Tensor seq_qstart, int num_seqs, int num_parts, int part_tokens, int n_q_heads, int n_kv_heads, "
@@ -489,6 +523,7 @@ TORCH_LIBRARY_IMPL(atta, CUDA, m) {
   m.impl("embed", &embed);
   m.impl("rope_cache", &rope_cache);
   m.impl("attention_prefill", &attention_prefill);
+  m.impl("flash_prefill", &flash_prefill);
   m.impl("attention_decode", &attention_decode);
   m.impl("sample", &sample);
   m.impl("skinny_gemm", &skinny_gemm);

@@ -1,0 +1,359 @@
+// Prefill flash attention over the paged KV cache, LDS-staged K/V tiles on 32x32x16 MFMA
+// (replaces the attention vLLM runs under engine.generate(), reference
+// llm/serve_llm.py:527-531).  Varlen batches, causal with a context offset (chunked prefill
+// and prefix-cache hits: query token i of a sequence sits at position kvlen - qlen + i),
+// GQA G = Hq / Hkv in {1, 2, 4, 8}, head_dim 128, bf16 / fp16.
+//
+// Work decomposition: grid (tiles, Hkv).  A workgroup = 4 waves owns 128 "columns" = the G
+// query heads of one KV head x 128 / G consecutive query tokens of one sequence; wave w owns
+// columns 32w..32w+31 (column c: token c / G, head c % G).  Every K/V tile is staged ONCE in
+// LDS per workgroup and read by all 128 columns (G x the reuse of a per-head kernel).
+//
+// Per 32-key block, per wave (cdna_hip_programming.md §3 "swapped QK^T"):
+//   S^T[32 keys x 32 cols] = K[32 x 128] . Q^T[128 x 32]       8 x mfma_f32_32x32x16
+//     A = K rows from LDS (16 B reads, rows padded to 272 B: conflict-free), B = Q (registers);
+//     the accumulator has the column on the lane, so the online-softmax row statistics are
+//     lane-local over 16 registers plus one xor-32 exchange;
+//   O^T[128 x 32] += V^T[128 x 32 keys] . P^T[32 keys x 32]    8 x mfma_f32_32x32x16
+//     B = P^T straight from the S^T accumulator registers (pairs packed to 16 bit; the k order
+//     inside a step is permuted, and the V^T A-operand reads follow the same permutation),
+//     A = V^T rows from LDS (two 8 B reads per fragment; rows padded to 72 B: conflict-free).
+// 64-key blocks (two 32-key sub-tiles).  O^T is rescaled only when a running max moved.
+// Pipelining: the next block's K/V are loaded global -> registers while the current block
+// computes, then written to the other LDS buffer; one workgroup barrier per block.  The
+// sequence's block-table slice is staged in LDS once so K/V addresses need no dependent
+// global load inside the loop.  Causal masking touches only the diagonal blocks.
+#include "common.h"
+#include "kernels.h"
+
+namespace atta {
+namespace fp {
+
+constexpr int kD = 128;
+constexpr int kNS = 2;                   // 32-key sub-tiles per block
+constexpr int kKB = 32 * kNS;            // keys per block
+constexpr int kKStride = kD + 8;         // K tile row: 272 B (16 B reads conflict-free)
+constexpr int kVStride = kKB + 4;        // V^T tile row: 136 B (8 B reads conflict-free)
+constexpr int kKTile = kKB * kKStride;   // elements
+constexpr int kVTile = kD * kVStride;
+constexpr int kBtLds = 2048;             // block-table entries staged in LDS
+constexpr float kNegInf = -__builtin_huge_valf();
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+
+template <typename T>
+struct Mf32;
+template <>
+struct Mf32<__bf16> {
+  typedef bf16x8 frag;
+  __device__ static __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <>
+struct Mf32<_Float16> {
+  typedef f16x8 frag;
+  __device__ static __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+};
+
+struct FlashParams {
+  uint16_t* out;            // [n_q_tokens, Hq, D] rows of out_stride
+  const uint16_t* q;        // [n_q_tokens, Hq, D] rows of q_stride
+  const uint16_t* k_cache;  // [nb, Hkv, BS, D]
+  const uint16_t* v_cache;  // [nb, Hkv, D, BS]
+  const int* block_tables;  // [S, bt_stride]
+  const int* seq_kvlen;
+  const int* seq_qstart;
+  const int* tile_seq;
+  const int* tile_qoff;
+  int num_tiles;
+  int64_t q_stride, out_stride;
+  int bt_stride, n_kv_heads, bs_shift;
+  float scale_log2;
+};
+
+template <typename T>
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return static_cast<uint32_t>(from_f32<T>(a)) | (static_cast<uint32_t>(from_f32<T>(b)) << 16);
+}
+
+template <typename T, int G>
+__global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
+  using MF = Mf32<T>;
+  using frag = typename MF::frag;
+  constexpr int kTokPerWave = 32 / G;
+  constexpr int kTokPerWg = 4 * kTokPerWave;
+  __shared__ __attribute__((aligned(16))) uint16_t lds_k[2][kKTile];
+  __shared__ __attribute__((aligned(16))) uint16_t lds_v[2][kVTile];
+  __shared__ int lds_bt[kBtLds];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int r = lane & 31;   // column within the wave / row within a 32-row operand
+  const int h = lane >> 5;   // lane half
+  // heaviest (latest-token) tiles first: tiles are emitted in token order per sequence
+  const int tile = p.num_tiles - 1 - static_cast<int>(blockIdx.x);
+  const int hk = blockIdx.y;
+  const int s = p.tile_seq[tile];
+  const int qoff = p.tile_qoff[tile];
+  const int kvlen = p.seq_kvlen[s];  // >= wg_end: every key this workgroup reads is below it
+  const int qstart = p.seq_qstart[s];
+  const int qlen = p.seq_qstart[s + 1] - qstart;
+  const int ctx0 = kvlen - qlen;
+  const int BS = 1 << p.bs_shift;
+  const int* bt = p.block_tables + static_cast<int64_t>(s) * p.bt_stride;
+
+  // this lane's column
+  const int c_tok = qoff + wid * kTokPerWave + r / G;
+  const int c_head = hk * G + r % G;
+  const bool c_valid = c_tok < qlen;
+  const int c_end = c_valid ? ctx0 + c_tok + 1 : 0;  // keys [0, c_end) are visible
+  // workgroup key range: up to the last valid token's causal limit
+  const int wg_last_tok = min(qoff + kTokPerWg, qlen) - 1;
+  const int wg_end = ctx0 + wg_last_tok + 1;
+  const int nblocks = (wg_end + kKB - 1) / kKB;
+  // wave key range (wave-uniform): blocks at or past it only need the wave at the barrier
+  const int w_last_tok = min(qoff + (wid + 1) * kTokPerWave, qlen) - 1;
+  const int w_end = w_last_tok >= qoff + wid * kTokPerWave ? ctx0 + w_last_tok + 1 : 0;
+  const int w_first = qoff + wid * kTokPerWave;  // first token: fully visible below ctx0+w_first+1
+
+  // ---- block table slice -> LDS -------------------------------------------------------
+  const int npages = min((wg_end + BS - 1) >> p.bs_shift, kBtLds);
+  for (int i = tid; i < npages; i += 256) lds_bt[i] = bt[i];
+
+  // ---- Q (B operand): Q[col r][16 st + 8 h .. +8], 8 k-steps over D ----------------------
+  frag qf[8];
+  {
+    const uint16_t* qp = p.q + static_cast<int64_t>(qstart + (c_valid ? c_tok : 0)) * p.q_stride +
+                         static_cast<int64_t>(c_head) * kD + 8 * h;
+#pragma unroll
+    for (int st = 0; st < 8; ++st)
+      qf[st] = c_valid ? *reinterpret_cast<const frag*>(qp + 16 * st) : frag{};
+  }
+  __syncthreads();  // lds_bt ready
+
+  // ---- global -> register staging of one K/V block --------------------------------------
+  // K tile: kKB x 16 chunks of 16 B, chunk c = (key c >> 4, dims 8 (c & 15));
+  // V^T tile: 128 x kKB / 8 chunks, chunk c = (d c / (kKB / 8), keys 8 (c % (kKB / 8)));
+  // thread t handles chunks t + 256 u
+  constexpr int kChunks = kKB * 16 / 256;   // per thread, per tensor
+  constexpr int kVq = kKB / 8;              // 8-key groups per V^T row
+  auto page_of = [&](int key) -> int {
+    const int i = key >> p.bs_shift;
+    return i < kBtLds ? lds_bt[i] : bt[i];
+  };
+  const int64_t head_elems = static_cast<int64_t>(BS) * kD;  // per (page, head)
+  u32x4 kr[kChunks], vr[kChunks];
+  auto load_block = [&](int kb) {
+#pragma unroll
+    for (int u = 0; u < kChunks; ++u) {
+      const int c = tid + 256 * u;
+      int key = kb * kKB + (c >> 4);
+      key = min(key, wg_end - 1);  // rows past the causal range are masked; stay in-table
+      const int pg = page_of(key);
+      const uint16_t* src = p.k_cache + (static_cast<int64_t>(pg) * p.n_kv_heads + hk) * head_elems +
+                            static_cast<int64_t>(key & (BS - 1)) * kD + 8 * (c & 15);
+      kr[u] = *reinterpret_cast<const u32x4*>(src);
+    }
+#pragma unroll
+    for (int u = 0; u < kChunks; ++u) {
+      const int c = tid + 256 * u;
+      int key = kb * kKB + 8 * (c % kVq);
+      key = min(key, (wg_end - 1) & ~7);  // 8-key groups never straddle a page (BS >= 16)
+      const int pg = page_of(key);
+      const uint16_t* src = p.v_cache + (static_cast<int64_t>(pg) * p.n_kv_heads + hk) * head_elems +
+                            static_cast<int64_t>(c / kVq) * BS + (key & (BS - 1));
+      vr[u] = *reinterpret_cast<const u32x4*>(src);
+    }
+  };
+  auto store_block = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < kChunks; ++u) {
+      const int c = tid + 256 * u;
+      *reinterpret_cast<u32x4*>(&lds_k[buf][(c >> 4) * kKStride + 8 * (c & 15)]) = kr[u];
+    }
+#pragma unroll
+    for (int u = 0; u < kChunks; ++u) {
+      const int c = tid + 256 * u;
+      uint16_t* dst = &lds_v[buf][(c / kVq) * kVStride + 8 * (c % kVq)];  // 8 B aligned rows
+      reinterpret_cast<u32x2*>(dst)[0] = u32x2{vr[u][0], vr[u][1]};
+      reinterpret_cast<u32x2*>(dst)[1] = u32x2{vr[u][2], vr[u][3]};
+    }
+  };
+
+  f32x16 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
+  float m_run = kNegInf, l_run = 0.f;
+
+  if (nblocks > 0) {
+    load_block(0);
+    store_block(0);
+  }
+  __syncthreads();
+
+  for (int kb = 0; kb < nblocks; ++kb) {
+    const int buf = kb & 1;
+    const bool more = kb + 1 < nblocks;
+    if (more) load_block(kb + 1);  // in flight during this block's MFMAs
+    const int k0 = kb * kKB;
+    if (k0 < w_end) {  // wave-uniform: the wave has visible keys in this block
+      const uint16_t* kl = lds_k[buf];
+      const uint16_t* vl = lds_v[buf];
+      // S^T = K . Q^T, one 32x32 accumulator per 32-key sub-tile
+      f32x16 sacc[kNS];
+#pragma unroll
+      for (int t = 0; t < kNS; ++t) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[t][i] = 0.f;
+#pragma unroll
+        for (int st = 0; st < 8; ++st) {
+          const frag kf =
+              *reinterpret_cast<const frag*>(kl + (32 * t + r) * kKStride + 16 * st + 8 * h);
+          sacc[t] = MF::mma(kf, qf[st], sacc[t]);
+        }
+      }
+      // mask (only blocks crossing the diagonal of the wave's first token, or kvlen)
+      const bool need_mask = k0 + kKB > ctx0 + w_first + 1;
+      float tmax = kNegInf;
+#pragma unroll
+      for (int t = 0; t < kNS; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = k0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+          float v = sacc[t][i] * p.scale_log2;
+          if (need_mask && key >= c_end) v = kNegInf;
+          sacc[t][i] = v;
+          tmax = fmaxf(tmax, v);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, kWave));
+      const float m_new = fmaxf(m_run, tmax);
+      const float m_use = (m_new == kNegInf) ? 0.f : m_new;
+      // rescale O only when some column's running max moved (wave-uniform skip: after the
+      // first blocks the max rarely changes)
+      if (__any(m_new != m_run)) {
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
+        l_run *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+      }
+      m_run = m_new;
+      float psum = 0.f;
+#pragma unroll
+      for (int t = 0; t < kNS; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float e = __builtin_amdgcn_exp2f(sacc[t][i] - m_use);
+          sacc[t][i] = e;
+          psum += e;
+        }
+      psum += __shfl_xor(psum, 32, kWave);
+      l_run += psum;
+      // P^T fragments per 16-key step: registers 8s..8s+7 of the sub-tile packed pairwise;
+      // O^T += V^T . P^T (A element j of half h = key 16 s + 8 (j >> 2) + 4 h + (j & 3))
+#pragma unroll
+      for (int t = 0; t < kNS; ++t) {
+        frag pf[2];
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          u32x4 w;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            w[j] = pack2<T>(sacc[t][8 * st + 2 * j], sacc[t][8 * st + 2 * j + 1]);
+          pf[st] = __builtin_bit_cast(frag, w);
+        }
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const uint16_t* vrow = vl + (32 * dt + r) * kVStride + 32 * t + 4 * h;
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            const u32x2 lo = *reinterpret_cast<const u32x2*>(vrow + 16 * st);
+            const u32x2 hi = *reinterpret_cast<const u32x2*>(vrow + 16 * st + 8);
+            const frag vf = __builtin_bit_cast(frag, u32x4{lo[0], lo[1], hi[0], hi[1]});
+            o[dt] = MF::mma(vf, pf[st], o[dt]);
+          }
+        }
+      }
+    }
+    if (more) store_block(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: O = O^T / l, lane (col r, half h) holds d = 32 dt + (i & 3) + 8 (i >> 2) + 4 h
+  if (c_valid) {
+    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    uint16_t* op = p.out + static_cast<int64_t>(qstart + c_tok) * p.out_stride +
+                   static_cast<int64_t>(c_head) * kD + 4 * h;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u32x2 w;
+        w[0] = pack2<T>(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
+        w[1] = pack2<T>(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+        *reinterpret_cast<u32x2*>(op + 32 * dt + 8 * g) = w;
+      }
+  }
+}
+
+template <typename T>
+static int launch(int G, dim3 grid, hipStream_t st, const FlashParams& p) {
+  switch (G) {
+    case 1: flash_prefill_kernel<T, 1><<<grid, 256, 0, st>>>(p); return 0;
+    case 2: flash_prefill_kernel<T, 2><<<grid, 256, 0, st>>>(p); return 0;
+    case 4: flash_prefill_kernel<T, 4><<<grid, 256, 0, st>>>(p); return 0;
+    case 8: flash_prefill_kernel<T, 8><<<grid, 256, 0, st>>>(p); return 0;
+    default: return -1;
+  }
+}
+
+}  // namespace fp
+}  // namespace atta
+
+using namespace atta;
+
+int atta_flash_prefill(void* out, const void* q, const void* k_cache, const void* v_cache,
+                       const int* block_tables, const int* seq_kvlen, const int* seq_qstart,
+                       const int* tile_seq, const int* tile_qoff, int num_tiles, int n_q_heads,
+                       int n_kv_heads, int head_dim, int block_size, int bt_stride,
+                       int64_t q_stride, int64_t out_stride, float scale, int dtype,
+                       hipStream_t stream) {
+  const int G = n_q_heads / n_kv_heads;
+  int shift = 0;
+  while ((1 << shift) < block_size) ++shift;
+  if (head_dim != fp::kD || (1 << shift) != block_size || block_size < 16) return -1;
+  if (n_q_heads % n_kv_heads || G > 8 || (G & (G - 1))) return -1;
+  // 16-byte row loads of q / stores of out need 8-element aligned row strides
+  if (q_stride % 8 || out_stride % 4) return -1;
+  if (num_tiles == 0) return 0;
+  fp::FlashParams prm{};
+  prm.out = static_cast<uint16_t*>(out);
+  prm.q = static_cast<const uint16_t*>(q);
+  prm.k_cache = static_cast<const uint16_t*>(k_cache);
+  prm.v_cache = static_cast<const uint16_t*>(v_cache);
+  prm.block_tables = block_tables;
+  prm.seq_kvlen = seq_kvlen;
+  prm.seq_qstart = seq_qstart;
+  prm.tile_seq = tile_seq;
+  prm.tile_qoff = tile_qoff;
+  prm.num_tiles = num_tiles;
+  prm.q_stride = q_stride;
+  prm.out_stride = out_stride;
+  prm.bt_stride = bt_stride;
+  prm.n_kv_heads = n_kv_heads;
+  prm.bs_shift = shift;
+  prm.scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid(num_tiles, n_kv_heads);
+  const int rc = dtype == 0 ? fp::launch<__bf16>(G, grid, stream, prm)
+                            : fp::launch<_Float16>(G, grid, stream, prm);
+  if (rc) return rc;
+  return static_cast<int>(hipGetLastError());
+}

@@ -32,6 +32,14 @@ int atta_attention_prefill(void* out, const void* q, const void* k_cache, const 
                            int bt_stride, int64_t q_stride, int64_t out_stride, float scale,
                            int dtype, hipStream_t stream);
 
+// LDS-staged flash attention for prefill (flash_prefill.hip): tiles of 128 / G query tokens.
+int atta_flash_prefill(void* out, const void* q, const void* k_cache, const void* v_cache,
+                       const int* block_tables, const int* seq_kvlen, const int* seq_qstart,
+                       const int* tile_seq, const int* tile_qoff, int num_tiles, int n_q_heads,
+                       int n_kv_heads, int head_dim, int block_size, int bt_stride,
+                       int64_t q_stride, int64_t out_stride, float scale, int dtype,
+                       hipStream_t stream);
+
 int atta_attention_decode(void* out, float* part_out, float* part_lse, const void* q,
                           const void* k_cache, const void* v_cache, const int* block_tables,
                           const int* seq_kvlen, const int* seq_qstart, int num_seqs,

@@ -1,0 +1,53 @@
+"""Prefill attention microbench on MI355X: flash (LDS-staged, 32x32x16 MFMA) vs v1, causal,
+one sequence of N tokens (plus a chunk-after-prefix case), Llama-3-8B (32/8) and 70B (64/8)
+head geometry.  Reports us and TFLOP/s (causal FLOPs = 2 * 2 * N^2/2 * D * Hq)."""
+import math
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "tests"))
+from agentic_traffic_testing_amd import ops  # noqa: E402
+from test_kernels_gpu import _make_paged, _tiles  # noqa: E402
+
+
+def timeit(fn, iters=20, reps=3):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    res = []
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        res.append(s.elapsed_time(e) / iters * 1000)
+    return statistics.median(res)
+
+
+def main():
+    dt = torch.bfloat16
+    print("== prefill attention (us / TFLOP/s)")
+    for hq, hkv in ((32, 8), (64, 8)):
+        for kv, ql in ((512, 512), (2600, 2600), (4096, 4096), (3000 + 700, 700), (8192, 8192)):
+            k, v, bt, kvlen, qstart, T = _make_paged([(kv, ql)], hkv, 16, dt)
+            q = torch.randn(T, hq, 128, dtype=dt, device="cuda")
+            flops = 4 * 128 * hq * (ql * (kv - ql) + ql * (ql + 1) / 2)
+            row = f"Hq={hq:2d} kv={kv:5d} q={ql:5d} |"
+            for impl in ("flash", "v1"):
+                ts, to = _tiles([(kv, ql)], ops.prefill_tile_tokens(hq // hkv, impl))
+                out = torch.empty_like(q)
+                t = timeit(lambda: ops.attention_prefill(q, k, v, bt, kvlen, qstart, ts, to,
+                                                         0.088, out=out, impl=impl))
+                row += f" {impl} {t:8.1f} us {flops / t / 1e6:6.1f} TF |"
+            print(row, flush=True)
+
+
+if __name__ == "__main__":
+    assert ops.native_available()
+    main()

@@ -118,27 +118,47 @@ def _make_paged(seqs, hkv, bs, dtype, nb_extra=8, seed=0):
     return k, v, bt.cuda(), kvlen.cuda(), qstart.cuda(), int(sum(qlens))
 
 
-@pytest.mark.parametrize("dtype", DT)
-@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 1), (4, 1), (16, 16)])
-@pytest.mark.parametrize("bs", [16, 32])
-def test_attention_prefill(dtype, hq, hkv, bs):
-    torch.manual_seed(4)
-    # (kvlen, qlen): full prompt, chunk after cached prefix, single token, long-ish
-    seqs = [(53, 53), (300, 77), (17, 1), (640, 640), (129, 2)]
-    k, v, bt, kvlen, qstart, T = _make_paged(seqs, hkv, bs, dtype)
-    q = torch.randn(T, hq, 128, dtype=dtype, device="cuda")
-    tile = ops.PREFILL_TILE_TOKENS[hq // hkv]
+def _tiles(seqs, tile):
     ts, to = [], []
     for i, (_, ql) in enumerate(seqs):
         for off in range(0, ql, tile):
             ts.append(i)
             to.append(off)
-    ts = torch.tensor(ts, dtype=torch.int32, device="cuda")
-    to = torch.tensor(to, dtype=torch.int32, device="cuda")
+    return (torch.tensor(ts, dtype=torch.int32, device="cuda"),
+            torch.tensor(to, dtype=torch.int32, device="cuda"))
+
+
+@pytest.mark.parametrize("impl", ["flash", "v1"])
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 1), (4, 1), (16, 16)])
+@pytest.mark.parametrize("bs", [16, 32])
+def test_attention_prefill(impl, dtype, hq, hkv, bs):
+    torch.manual_seed(4)
+    # (kvlen, qlen): full prompt, chunk after cached prefix, single token, long-ish
+    seqs = [(53, 53), (300, 77), (17, 1), (640, 640), (129, 2)]
+    k, v, bt, kvlen, qstart, T = _make_paged(seqs, hkv, bs, dtype)
+    q = torch.randn(T, hq, 128, dtype=dtype, device="cuda")
+    ts, to = _tiles(seqs, ops.prefill_tile_tokens(hq // hkv, impl))
     scale = 1 / math.sqrt(128)
-    bt_ref = bt.clamp(min=0)
-    exp = ref.paged_attention(q, k, v, bt_ref, kvlen, qstart, scale)
-    got = ops.attention_prefill(q, k, v, bt, kvlen, qstart, ts, to, scale)
+    exp = ref.paged_attention(q, k, v, bt.clamp(min=0), kvlen, qstart, scale)
+    got = ops.attention_prefill(q, k, v, bt, kvlen, qstart, ts, to, scale, impl=impl)
+    close(got, exp, 1.5e-2, 2e-2)
+
+
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8)])
+def test_flash_prefill_long_chunked(hq, hkv):
+    """2.6k-token prompt (the fan-out synthesis size) plus a chunk after a 3k cached prefix
+    and an 11k-context chunk (reference .env max_model_len 11000): the flash kernel's block
+    loop, diagonal masking and block-table staging stay exact."""
+    torch.manual_seed(6)
+    dt = torch.bfloat16
+    seqs = [(2600, 2600), (3000 + 700, 700), (11000, 300)]
+    k, v, bt, kvlen, qstart, T = _make_paged(seqs, hkv, 16, dt)
+    q = torch.randn(T, hq, 128, dtype=dt, device="cuda")
+    ts, to = _tiles(seqs, ops.prefill_tile_tokens(hq // hkv, "flash"))
+    scale = 1 / math.sqrt(128)
+    exp = ref.paged_attention(q, k, v, bt.clamp(min=0), kvlen, qstart, scale)
+    got = ops.attention_prefill(q, k, v, bt, kvlen, qstart, ts, to, scale, impl="flash")
     close(got, exp, 1.5e-2, 2e-2)
 
 
