@@ -93,6 +93,7 @@ class LLMEngine:
         self._rng = random.Random(cfg.seed)
         # async look-ahead decode: the step launched but not yet collected (see step())
         self._inflight: _Inflight | None = None
+        self._last_collect = 0.0
 
     # ------------------------------------------------------------------------------------
     def add_request(self, request_id: str, prompt_ids, sampling: SamplingParams,
@@ -179,7 +180,8 @@ class LLMEngine:
     def _collect(self, cur: "_Inflight") -> list[RequestOutput]:
         toks = self.runner.collect(cur.handle)
         now = time.perf_counter()
-        self.timing["execute"] += now - cur.t0
+        self.timing["execute"] += now - max(cur.t0, self._last_collect)
+        self._last_collect = now
         self.timing["steps"] += 1
         outs = []
         for (seq, idx, ncomp), tok in zip(cur.marks, toks):

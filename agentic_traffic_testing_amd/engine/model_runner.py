@@ -119,7 +119,8 @@ class ModelRunner:
             self.model.load_safetensors(weights_dir)
         else:
             self.model.init_random(seed=cfg.seed)
-        if self.is_cuda and ((cfg.fused_decode and cfg.preshuffle_decode_weights)
+        if self.is_cuda and ((cfg.fused_decode and cfg.preshuffle_decode_weights
+                              and self._room_for_decode_copies())
                              or cfg.quantization == "fp8"):
             self.model.prepare_decode_weights()
         self.load_seconds = time.perf_counter() - t0
@@ -161,6 +162,7 @@ class ModelRunner:
         self.tok_host = [torch.zeros(max(cfg.max_num_seqs, 256), dtype=torch.int64,
                                      pin_memory=pin) for _ in range(2)]
         self._tok_done = [torch.cuda.Event() if self.is_cuda else None for _ in range(2)]
+        self._last_collect = 0.0
         nkv = self.model.n_kv_heads
         self.part_out = torch.empty(self.max_seqs * nkv * alloc_parts * 16 * 128,
                                     dtype=torch.float32, device=self.device)
@@ -192,6 +194,20 @@ class ModelRunner:
         self.steps = 0
         self.graph_steps = 0
         self.timing = {"graph_prep": 0.0, "graph_run": 0.0}
+
+    def _room_for_decode_copies(self) -> bool:
+        """The pre-shuffled decode copies double the 16-bit weights (16 GB for Llama-3.1-8B);
+        Llama-3-70B bf16 on ONE GPU (141 GB) cannot afford a second copy next to its KV cache,
+        so it decodes from the row-major weights instead."""
+        need = self.model.decode_copy_bytes()
+        torch.cuda.synchronize(self.device)
+        free, total = torch.cuda.mem_get_info(self.device)
+        keep = max(int(0.15 * total), 24 << 30)  # KV cache + activations + graphs
+        if need > free - keep:
+            print(f"[atta] skipping pre-shuffled decode weights: {need / 2**30:.1f} GiB needed, "
+                  f"{free / 2**30:.1f} GiB free (row-major decode GEMVs)", flush=True)
+            return False
+        return True
 
     # ------------------------------------------------------------------------------------
     def _alloc_kv(self):
@@ -402,8 +418,12 @@ class ModelRunner:
         ev = self._tok_done[h["slot"]]
         if ev is not None:
             ev.synchronize()
+        now = time.perf_counter()
         if h["graph"]:
-            self.timing["graph_run"] += time.perf_counter() - h["t_launch"]
+            # pipelined steps overlap: charge each step from the later of its launch and the
+            # previous collect, so graph_run / graph_steps stays the per-step wall time
+            self.timing["graph_run"] += now - max(h["t_launch"], self._last_collect)
+        self._last_collect = now
         return self.tok_host[h["slot"]][:h["n"]].numpy().copy()
 
     def _run(self, hdr, sampler=None, worker: bool = False):

