@@ -285,8 +285,7 @@ class LlamaModel:
             return ops.linear(x, w, residual=residual)
         y = ops.linear_fp8(x, w, scale)
         if residual is not None:
-            residual.copy_((y.float() + residual.float()).to(residual.dtype))
-            return residual
+            return residual.add_(y)
         return y
 
     def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
@@ -306,9 +305,16 @@ class LlamaModel:
         residual = ops.embed(self.embed, input_ids, prev_tokens, feed_prev)
         T = residual.shape[0]
         nq, nkv, D = self.n_heads, self.n_kv_heads, self.head_dim
+        # fp8 weights on the GPU: every projection is ONE fp8 GEMM with row-wise scales whose
+        # activation operand comes quantised out of the norm / SiLU-mul kernel that produced it
+        fp8 = self.quant == "fp8" and self.device.type == "cuda"
+        dt = residual.dtype
         for li, L in enumerate(self.layers):
-            x = ops.rms_norm(residual, L.input_norm, eps)
-            qkv = self._proj(x, L.qkv, L.qkv_s)
+            if fp8:
+                xq, xs = ops.quant_rows_fp8(residual, ops.QUANT_NORM, L.input_norm, eps)
+                qkv = ops.gemm_fp8(xq, xs, L.qkv, L.qkv_s, dt)
+            else:
+                qkv = self._proj(ops.rms_norm(residual, L.input_norm, eps), L.qkv, L.qkv_s)
             q = ops.rope_cache(qkv, md.positions, md.slot_mapping, self.cos_sin, k_caches[li],
                                v_caches[li], nq, nkv, D)
             attn = torch.empty_like(q)
@@ -320,6 +326,14 @@ class LlamaModel:
                 ops.attention_prefill(q, k_caches[li], v_caches[li], md.block_tables,
                                       md.seq_kvlen, md.seq_qstart, md.tile_seq, md.tile_qoff,
                                       self.scale, out=attn)
+            if fp8:
+                aq, as_ = ops.quant_rows_fp8(attn.view(T, nq * D))
+                residual.add_(self._all_reduce(ops.gemm_fp8(aq, as_, L.o, L.o_s, dt)))
+                xq, xs = ops.quant_rows_fp8(residual, ops.QUANT_NORM, L.post_norm, eps)
+                gu = ops.gemm_fp8(xq, xs, L.gate_up, L.gate_up_s, dt)
+                aq, as_ = ops.quant_rows_fp8(gu, ops.QUANT_SILU)
+                residual.add_(self._all_reduce(ops.gemm_fp8(aq, as_, L.down, L.down_s, dt)))
+                continue
             self._proj_residual(attn.view(T, nq * D), L.o, L.o_s, residual)
             x = ops.rms_norm(residual, L.post_norm, eps)
             gu = self._proj(x, L.gate_up, L.gate_up_s)

@@ -364,30 +364,52 @@ def _rowmap_index(N: int, rowmap: str, dev):
     raise ValueError(f"unknown rowmap {rowmap}")
 
 
-_SCALED_MM_OK: bool | None = None
+# fp8 activation quantisation modes (ops/csrc/quant_fp8.hip)
+QUANT_NORM, QUANT_SILU, QUANT_PLAIN = 0, 1, 2
+
+
+def quant_rows_fp8(x: torch.Tensor, mode: int = QUANT_PLAIN, w: torch.Tensor | None = None,
+                   eps: float = 1e-5) -> tuple[torch.Tensor, torch.Tensor]:
+    """Row-wise e4m3fn quantisation of ``x`` (``QUANT_PLAIN``), of rmsnorm(x) * w
+    (``QUANT_NORM``) or of silu(gate) * up for gate | up rows (``QUANT_SILU``), fused in one
+    HIP kernel.  Returns (uint8 codes [M, width], fp32 scales [M, 1])."""
+    M = x.shape[0]
+    width = x.shape[1] // 2 if mode == QUANT_SILU else x.shape[1]
+    if not x.is_cuda:
+        if mode == QUANT_NORM:
+            v = ref.rms_norm(x, w, eps).float()
+        elif mode == QUANT_SILU:
+            v = ref.silu_and_mul(x).float()
+        else:
+            v = x.float()
+        s = (v.abs().amax(dim=1, keepdim=True) / FP8_MAX)
+        s = torch.where(s > 0, s, torch.ones_like(s))
+        q = (v / s).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).view(torch.uint8)
+        return q, s
+    q = torch.empty(M, width, dtype=torch.uint8, device=x.device)
+    s = torch.empty(M, 1, dtype=torch.float32, device=x.device)
+    _native().quant_rows_fp8(q, s, x, w if mode == QUANT_NORM else None, mode, eps)
+    return q, s
+
+
+def gemm_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,
+             out_dtype=torch.bfloat16) -> torch.Tensor:
+    """y[m, n] = xs[m] ws[n] sum_k fp8(xq)[m, k] fp8(wq)[n, k]: one hipBLASLt fp8 GEMM with
+    row-wise scales on both operands (torch._scaled_mm, CDNA4 fp8 MFMA), bf16 out, no torch
+    passes around it.  Failures raise: there is no silent dequantise fallback on a GPU."""
+    if not xq.is_cuda:
+        x = xq.view(torch.float8_e4m3fn).float() * xs
+        w = wq.view(torch.float8_e4m3fn).float() * ws.reshape(-1, 1)
+        return (x @ w.t()).to(out_dtype)
+    return torch._scaled_mm(xq.view(torch.float8_e4m3fn), wq.view(torch.float8_e4m3fn).t(),
+                            scale_a=xs, scale_b=ws.reshape(1, -1), out_dtype=out_dtype)
 
 
 def linear_fp8(x: torch.Tensor, q: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
-    """Prefill-sized y = x @ dequant(q).T with row-major fp8 weights: per-tensor dynamic
-    activation scale, hipBLASLt fp8 GEMM (torch._scaled_mm, fp8 MFMA), per-row weight scale
-    applied to the bf16 output.  Falls back to dequantise + GEMM where _scaled_mm is absent."""
-    global _SCALED_MM_OK
-    if x.is_cuda and _SCALED_MM_OK is not False:
-        try:
-            sx = (x.float().abs().amax() / FP8_MAX).clamp_min(1e-12)
-            xq = (x.float() / sx).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
-            one = torch.ones((), device=x.device, dtype=torch.float32)
-            y = torch._scaled_mm(xq, q.view(torch.float8_e4m3fn).t(), scale_a=sx, scale_b=one,
-                                 out_dtype=x.dtype)
-            _SCALED_MM_OK = True
-            return (y.float() * scale[None, :]).to(x.dtype)
-        except (RuntimeError, TypeError) as e:
-            if _SCALED_MM_OK:
-                raise
-            _SCALED_MM_OK = False
-            print(f"[atta] torch._scaled_mm unavailable for fp8 prefill ({e}); "
-                  "dequantising per GEMM", flush=True)
-    return torch.nn.functional.linear(x, dequantize_fp8(q, scale, x.dtype))
+    """y = x @ dequant(q).T for 16-bit activations and row-major fp8 weights: the fused
+    row-wise activation quantiser, then ``gemm_fp8``."""
+    xq, xs = quant_rows_fp8(x, QUANT_PLAIN)
+    return gemm_fp8(xq, xs, q, scale, x.dtype)
 
 
 def _need_cuda(x, preshuffled):

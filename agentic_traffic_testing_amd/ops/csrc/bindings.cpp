@@ -342,6 +342,38 @@ void fused_lm_head_sample(at::Tensor tokens, at::Tensor keys, const at::Tensor& 
            "fused_lm_head_sample");
 }
 
+// Row-wise fp8 activation quantisation fused into norm / SiLU-mul / plain rows.
+void quant_rows_fp8(at::Tensor q, at::Tensor scale, const at::Tensor& x,
+                    const c10::optional<at::Tensor>& w, int64_t mode, double eps) {
+  check_dev(x, "x");
+  check_dev(q, "q");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "quant_rows_fp8: mode 0 (norm) / 1 (silu) / 2 (plain)");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && q.dim() == 2 && q.stride(1) == 1 &&
+                  q.scalar_type() == at::kByte,
+              "quant_rows_fp8: 2-D rows, uint8 q");
+  const int64_t width = q.size(1);
+  TORCH_CHECK(q.size(0) == x.size(0) && x.size(1) == (mode == 1 ? 2 * width : width),
+              "quant_rows_fp8: shapes");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.is_contiguous() &&
+                  scale.numel() >= x.size(0) && scale.is_cuda(),
+              "quant_rows_fp8: fp32 scale [rows]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(q.data_ptr()) % 8 == 0,
+              "quant_rows_fp8: 16-byte aligned x rows, 8-byte aligned q rows");
+  const void* wp = nullptr;
+  if (mode == 0) {
+    TORCH_CHECK(w.has_value() && w->numel() == width && w->scalar_type() == x.scalar_type() &&
+                    w->is_cuda() && w->is_contiguous(),
+                "quant_rows_fp8: norm weight [width]");
+    wp = w->data_ptr();
+  }
+  const at::DeviceGuard g(x.device());
+  check_rc(atta_quant_rows_fp8(q.data_ptr(), scale.data_ptr<float>(), x.data_ptr(), wp,
+                               x.size(0), width, x.stride(0), q.stride(0), mode,
+                               static_cast<float>(eps), dtype_code(x), cur_stream()),
+           "quant_rows_fp8");
+}
+
 // Registers the split-K workspace of the skinny GEMVs on ws's device.  The tensors must
 // outlive every launch (and captured graph) that uses a split > 1; counters start zeroed.
 void set_splitk_workspace(const at::Tensor& ws, const at::Tensor& counters) {
@@ -484,6 +516,8 @@ TORCH_LIBRARY(atta, m) {
   m.def("fused_gate_up_silu(Tensor(a!) out, Tensor x, Tensor w, float eps, int waves, "
         "bool preshuffled=False, Tensor? w_scale=None, int ksplit=1) -> ()");
   m.def("set_splitk_workspace(Tensor ws, Tensor counters) -> ()");
+  m.def("quant_rows_fp8(Tensor(a!) q, Tensor(b!) scale, Tensor x, Tensor? w, int mode, "
+        "float eps) -> ()");
   m.def(
       "fused_lm_head_sample(Tensor(a!) tokens, Tensor(b!) keys, Tensor x, Tensor w, float eps, "
       "Tensor temperature, Tensor seeds, Tensor steps, int finalize, int vocab_offset, "
@@ -532,6 +566,7 @@ TORCH_LIBRARY_IMPL(atta, CUDA, m) {
   m.impl("fused_lm_head_sample", &fused_lm_head_sample);
   m.impl("sample_finalize", &sample_finalize);
   m.impl("set_splitk_workspace", &set_splitk_workspace);
+  m.impl("quant_rows_fp8", &quant_rows_fp8);
   m.impl("attention_decode_v2", &attention_decode_v2);
   m.impl("skinny_variant", &skinny_variant);
 }

@@ -88,6 +88,13 @@ int atta_attention_decode_v2(void* out, float* part_out, float* part_lse, int* c
 int atta_skinny_variant(void* y, const void* x, const void* w, int M, int N, int K,
                         int variant, hipStream_t stream);
 
+// Row-wise e4m3fn activation quantisation (quant_fp8.hip): mode 0 = rmsnorm(x) * w,
+// 1 = silu(gate) * up (x rows hold gate | up, width = I), 2 = x.  q [rows, width] uint8,
+// scale [rows] fp32 (dequant: value = fp8 * scale).
+int atta_quant_rows_fp8(void* q, float* scale, const void* x, const void* w, int rows, int width,
+                        int64_t x_stride, int64_t q_stride, int mode, float eps, int dtype,
+                        hipStream_t stream);
+
 // ---- one-shot IPC all-reduce (allreduce.hip) ---------------------------------------------
 size_t atta_ar_buffer_bytes(int64_t max_elems, int elem_bytes);
 int atta_ar_alloc(void** ptr, size_t bytes);

@@ -543,3 +543,41 @@ def test_fp8_prefill_linear():
     # activation fp8 rounding dominates: relative error of a few percent of the row scale
     err = (got.float() - exp).abs().max() / exp.abs().max()
     assert float(err) < 0.08
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("m,width", [(1, 4096), (37, 8192), (300, 14336)])
+def test_quant_rows_fp8(mode, m, width):
+    """Fused row-wise e4m3fn quantisation (norm / silu-mul / plain) vs the fp32 reference:
+    scales match, codes dequantise to the reference values within e4m3 rounding."""
+    torch.manual_seed(40 + mode)
+    dt = torch.bfloat16
+    x = torch.randn(m, 2 * width if mode == 1 else width, dtype=dt, device="cuda") * 3
+    x[0] = 0 if mode == 2 else x[0]  # an all-zero row must not divide by zero
+    w = (1 + 0.1 * torch.randn(width, dtype=dt, device="cuda")) if mode == 0 else None
+    q, s = ops.quant_rows_fp8(x, mode, w, 1e-5)
+    qr, sr = ops.quant_rows_fp8(x.cpu(), mode, None if w is None else w.cpu(), 1e-5)
+    close(s.cpu(), sr, 0.0, 2e-2)
+    deq = q.view(torch.float8_e4m3fn).float().cpu() * s.cpu()
+    ref_v = qr.view(torch.float8_e4m3fn).float() * sr
+    # e4m3 has 3 mantissa bits: the reference rounds its normalised values to bf16 first,
+    # so a value on a code boundary may land one code step (<= 1/8 relative) away
+    err = (deq - ref_v).abs()
+    assert bool((err <= 0.14 * ref_v.abs() + s.cpu()).all()), float(err.max())
+    assert bool((deq.abs() <= 448 * s.cpu() * 1.0001).all())
+
+
+@pytest.mark.parametrize("m", [1, 7, 64, 300])
+def test_gemm_fp8_rowwise(m):
+    """Row-wise-scaled fp8 GEMM (hipBLASLt via torch._scaled_mm) == fp32 GEMM of the
+    dequantised operands."""
+    torch.manual_seed(41)
+    x = torch.randn(m, 4096, dtype=torch.bfloat16, device="cuda")
+    w = torch.randn(1024, 4096, dtype=torch.bfloat16, device="cuda") * 0.05
+    wq, ws = ops.quantize_fp8(w)
+    xq, xs = ops.quant_rows_fp8(x)
+    got = ops.gemm_fp8(xq, xs, wq, ws)
+    exp = (xq.view(torch.float8_e4m3fn).float() * xs) @ \
+        (wq.view(torch.float8_e4m3fn).float() * ws[:, None]).t()
+    err = (got.float() - exp).abs().max() / exp.abs().max()
+    assert float(err) < 1e-2
