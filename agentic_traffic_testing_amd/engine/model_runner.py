@@ -329,6 +329,10 @@ class ModelRunner:
                            prev_tokens=self.ws["tokens"] if decode_only else None,
                            feed_prev=v["feed_prev"] if decode_only else None)
         last = hidden.index_select(0, v["logits_idx"])
+        if special_sampling is None and m.decode_fusable(last.shape[0]) and \
+                last.shape[0] <= self.max_seqs and m.hidden_fusable():
+            # fused LM head + Gumbel-max sampler on the (already normalised) last rows
+            return m.sample_rows(last, 0.0, v["temperature"], v["seeds"], v["steps"], self.ws)
         logits = m.compute_logits(last)
         if special_sampling is not None:
             return special_sampling(logits)

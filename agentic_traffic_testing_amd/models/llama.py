@@ -309,9 +309,14 @@ class LlamaModel:
         # activation operand comes quantised out of the norm / SiLU-mul kernel that produced it
         fp8 = self.quant == "fp8" and self.device.type == "cuda"
         dt = residual.dtype
+        pending = None  # fp8: the previous down_proj output, added by the next norm kernel
         for li, L in enumerate(self.layers):
             if fp8:
-                xq, xs = ops.quant_rows_fp8(residual, ops.QUANT_NORM, L.input_norm, eps)
+                if pending is None:
+                    xq, xs = ops.quant_rows_fp8(residual, ops.QUANT_NORM, L.input_norm, eps)
+                else:
+                    xq, xs = ops.quant_rows_fp8(pending, ops.QUANT_ADDNORM, L.input_norm, eps,
+                                                residual)
                 qkv = ops.gemm_fp8(xq, xs, L.qkv, L.qkv_s, dt)
             else:
                 qkv = self._proj(ops.rms_norm(residual, L.input_norm, eps), L.qkv, L.qkv_s)
@@ -328,17 +333,19 @@ class LlamaModel:
                                       self.scale, out=attn)
             if fp8:
                 aq, as_ = ops.quant_rows_fp8(attn.view(T, nq * D))
-                residual.add_(self._all_reduce(ops.gemm_fp8(aq, as_, L.o, L.o_s, dt)))
-                xq, xs = ops.quant_rows_fp8(residual, ops.QUANT_NORM, L.post_norm, eps)
+                y = self._all_reduce(ops.gemm_fp8(aq, as_, L.o, L.o_s, dt))
+                xq, xs = ops.quant_rows_fp8(y, ops.QUANT_ADDNORM, L.post_norm, eps, residual)
                 gu = ops.gemm_fp8(xq, xs, L.gate_up, L.gate_up_s, dt)
                 aq, as_ = ops.quant_rows_fp8(gu, ops.QUANT_SILU)
-                residual.add_(self._all_reduce(ops.gemm_fp8(aq, as_, L.down, L.down_s, dt)))
+                pending = self._all_reduce(ops.gemm_fp8(aq, as_, L.down, L.down_s, dt))
                 continue
             self._proj_residual(attn.view(T, nq * D), L.o, L.o_s, residual)
             x = ops.rms_norm(residual, L.post_norm, eps)
             gu = self._proj(x, L.gate_up, L.gate_up_s)
             a = ops.silu_and_mul(gu)
             self._proj_residual(a, L.down, L.down_s, residual)
+        if pending is not None:
+            return ops.fused_add_rms_norm(pending, residual, self.norm, eps)
         return ops.rms_norm(residual, self.norm, eps)
 
     def _proj_residual(self, x, w, scale, residual):
@@ -354,6 +361,10 @@ class LlamaModel:
         return (self.device.type == "cuda" and num_tokens <= ops.SKINNY_MAX_M
                 and self.cfg.hidden_size % step == 0 and self.inter % step == 0
                 and (self.n_heads * self.head_dim) % step == 0)
+
+    def hidden_fusable(self) -> bool:
+        """The LM-head GEMV streams K = hidden in 128-wide (16-bit) wave steps."""
+        return self.device.type == "cuda" and self.cfg.hidden_size % 128 == 0
 
     def forward_decode(self, input_ids: torch.Tensor, md: AttnMeta, k_caches, v_caches, ws: dict,
                        temperature, seeds, steps, prev_tokens=None,
@@ -402,20 +413,26 @@ class LlamaModel:
                 residual.add_(self._all_reduce(ops.linear(act, L.down_ps if ps else L.down,
                                                           preshuffled=ps, w_scale=L.down_s,
                                                           ksplit=None, proj="down")))
+        return self.sample_rows(residual, eps, temperature, seeds, steps, ws)
+
+    def sample_rows(self, x, eps, temperature, seeds, steps, ws) -> torch.Tensor:
+        """[final RMSNorm (eps > 0) +] LM head + sampler for <= 32 rows without materialising
+        logits; tokens land in ws["tokens"][:B] on every rank (an async look-ahead step embeds
+        them from there).  Used by the fused decode step and for the last-token rows of
+        prefill steps (their rows are already normalised: eps = 0)."""
+        B = x.shape[0]
         lm_ps = self.lm_head_ps is not None
         lm = self.lm_head_ps if lm_ps else self.lm_head
         if self.tp_size == 1:
-            return ops.decode_lm_head_sample(residual, lm, eps, temperature, seeds, steps,
-                                             ws["keys"], tokens=ws["tokens"][:B],
-                                             preshuffled=lm_ps)
+            return ops.decode_lm_head_sample(x, lm, eps, temperature, seeds, steps, ws["keys"],
+                                             tokens=ws["tokens"][:B], preshuffled=lm_ps)
         # TP: each rank samples its vocab shard down to one packed key per row (global ids,
         # so the Gumbel noise equals TP=1's); one int64 MAX all-reduce picks the winner
-        keys = ops.decode_lm_head_sample(residual, lm, eps, temperature, seeds, steps,
-                                         ws["keys"], tokens=ws["tp_keys"][:B], finalize="key",
+        keys = ops.decode_lm_head_sample(x, lm, eps, temperature, seeds, steps, ws["keys"],
+                                         tokens=ws["tp_keys"][:B], finalize="key",
                                          vocab_offset=self.tp_rank * self.vocab_shard,
                                          preshuffled=lm_ps)
         self.tp_group.all_reduce_max(keys)
-        # tokens land in ws["tokens"] on every rank (an async look-ahead step embeds them)
         toks = ws["tokens"][:B]
         toks.copy_(ops.key_to_token(keys))
         return toks

@@ -365,17 +365,22 @@ def _rowmap_index(N: int, rowmap: str, dev):
 
 
 # fp8 activation quantisation modes (ops/csrc/quant_fp8.hip)
-QUANT_NORM, QUANT_SILU, QUANT_PLAIN = 0, 1, 2
+QUANT_NORM, QUANT_SILU, QUANT_PLAIN, QUANT_ADDNORM = 0, 1, 2, 3
 
 
 def quant_rows_fp8(x: torch.Tensor, mode: int = QUANT_PLAIN, w: torch.Tensor | None = None,
-                   eps: float = 1e-5) -> tuple[torch.Tensor, torch.Tensor]:
+                   eps: float = 1e-5, residual: torch.Tensor | None = None
+                   ) -> tuple[torch.Tensor, torch.Tensor]:
     """Row-wise e4m3fn quantisation of ``x`` (``QUANT_PLAIN``), of rmsnorm(x) * w
-    (``QUANT_NORM``) or of silu(gate) * up for gate | up rows (``QUANT_SILU``), fused in one
+    (``QUANT_NORM``), of silu(gate) * up for gate | up rows (``QUANT_SILU``), or - with
+    ``QUANT_ADDNORM`` - ``residual += x`` (in place) then rmsnorm(residual) * w, fused in one
     HIP kernel.  Returns (uint8 codes [M, width], fp32 scales [M, 1])."""
     M = x.shape[0]
     width = x.shape[1] // 2 if mode == QUANT_SILU else x.shape[1]
     if not x.is_cuda:
+        if mode == QUANT_ADDNORM:
+            residual.copy_((x.float() + residual.float()).to(residual.dtype))
+            x, mode = residual, QUANT_NORM
         if mode == QUANT_NORM:
             v = ref.rms_norm(x, w, eps).float()
         elif mode == QUANT_SILU:
@@ -388,7 +393,8 @@ def quant_rows_fp8(x: torch.Tensor, mode: int = QUANT_PLAIN, w: torch.Tensor | N
         return q, s
     q = torch.empty(M, width, dtype=torch.uint8, device=x.device)
     s = torch.empty(M, 1, dtype=torch.float32, device=x.device)
-    _native().quant_rows_fp8(q, s, x, w if mode == QUANT_NORM else None, mode, eps)
+    _native().quant_rows_fp8(q, s, x, w if mode in (QUANT_NORM, QUANT_ADDNORM) else None, mode,
+                             eps, residual if mode == QUANT_ADDNORM else None)
     return q, s
 
 

@@ -132,6 +132,175 @@ __global__ void __launch_bounds__(kThreads) oneshot_kernel(Params p, const uint1
   if (threadIdx.x == 0) counters[b] = gen;
 }
 
+// ---- two-shot (reduce-scatter + all-gather) for prefill-sized messages ------------------
+// Per rank, per call: (W-1)/W of the message leaves over xGMI twice instead of (W-1) whole
+// copies (one-shot), so the link time stays flat in W - the bandwidth-optimal shape of a ring
+// with 2 hops instead of 2(W-1).  Buffer of one rank (separate allocation, same uncached
+// memory and generation scheme as the one-shot kernel):
+//   [flags1 : 2 parities x kMaxRanks x k2Blocks]  phase-1 "my copy of your chunk landed"
+//   [flags2 : 2 parities x kMaxRanks x k2Blocks]  phase-2 "my reduced chunk landed"
+//   [counters: k2Blocks + 1 error word]
+//   [slot1 : 2 parities x W x chunk_max]   peers' copies of MY chunk
+//   [slot2 : 2 parities x W x chunk_max]   every rank's reduced chunk
+// Block b owns sub-range b of every chunk; chunk c = ranks' elements [c*chunk, (c+1)*chunk).
+// Reuse of parity g & 1 at call g + 2 is safe for the argument of the one-shot kernel: a
+// rank enters call g + 2 only after its call g + 1 saw every peer's phase-1 flags, which
+// peers raise only after their call g finished (stream order).
+constexpr int k2Blocks = 64;
+constexpr size_t k2FlagWords = 2 * kMaxRanks * k2Blocks;
+constexpr size_t k2HeaderBytes = 64 * 1024;
+
+struct Params2 {
+  uint8_t* base[kMaxRanks];
+  int rank, world;
+  int64_t chunk_max;  // elements per (parity, src) slot
+};
+
+__device__ __forceinline__ uint32_t* flag2_ptr(uint8_t* base, int phase, int par, int src,
+                                               int blk) {
+  return reinterpret_cast<uint32_t*>(base) + phase * k2FlagWords +
+         (par * kMaxRanks + src) * k2Blocks + blk;
+}
+template <int W>
+__device__ __forceinline__ uint16_t* slot2_ptr(uint8_t* base, int region, int par, int src,
+                                               int64_t chunk_max) {
+  return reinterpret_cast<uint16_t*>(base + k2HeaderBytes) +
+         ((region * 2 + par) * W + src) * chunk_max;
+}
+
+template <int W>
+__device__ __forceinline__ void raise_and_wait(uint8_t* const* bases, uint8_t* mine, int phase,
+                                               int par, int me, int b, uint32_t gen,
+                                               uint32_t* errw) {
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x < W) {
+    __hip_atomic_store(flag2_ptr(bases[threadIdx.x], phase, par, me, b), gen, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* f = flag2_ptr(mine, phase, par, threadIdx.x, b);
+    uint32_t spins = 0;  // bounded: a dead peer records itself in the error word
+    while (static_cast<int32_t>(__hip_atomic_load(f, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_SYSTEM) - gen) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 25)) {
+        atomicOr(errw, 1u << threadIdx.x);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+}
+
+template <typename T, int W>
+__global__ void __launch_bounds__(kThreads) twoshot_kernel(Params2 p, const uint16_t* x,
+                                                           uint16_t* y, int64_t n) {
+  using V = Pack8;
+  const int b = blockIdx.x;
+  const int me = p.rank;
+  uint8_t* mine = p.base[me];
+  uint32_t* counters = reinterpret_cast<uint32_t*>(mine) + 2 * k2FlagWords;
+  __shared__ uint32_t gen_s;
+  if (threadIdx.x == 0) gen_s = counters[b] + 1;
+  __syncthreads();
+  const uint32_t gen = gen_s;
+  const int par = gen & 1;
+
+  int64_t chunk = (n + W - 1) / W;
+  chunk = (chunk + 7) & ~int64_t(7);
+  int64_t sub = (chunk + k2Blocks - 1) / k2Blocks;
+  sub = (sub + 7) & ~int64_t(7);
+  const int64_t off = b * sub < chunk ? b * sub : chunk;   // within a chunk
+  const int64_t len = off + sub < chunk ? sub : chunk - off;
+  // elements [lo, hi) of chunk c that exist in the message
+  auto span = [&](int c, int64_t& lo, int64_t& hi) {
+    lo = c * chunk + off;
+    hi = lo + len;
+    if (hi > n) hi = n;
+    if (lo > hi) lo = hi;
+  };
+
+  // 1) scatter: my copy of chunk q (sub-range b) -> rank q's slot1(par, me)
+#pragma unroll
+  for (int q = 0; q < W; ++q) {
+    int64_t lo, hi;
+    span(q, lo, hi);
+    uint16_t* dst = slot2_ptr<W>(p.base[q], 0, par, me, p.chunk_max) + off - lo;
+    for (int64_t i = lo + 8 * threadIdx.x; i < hi; i += 8 * kThreads) {
+      if (i + 8 <= hi)
+        *reinterpret_cast<V*>(dst + i) = *reinterpret_cast<const V*>(x + i);
+      else
+        for (int64_t j = i; j < hi; ++j) dst[j] = x[j];
+    }
+  }
+  raise_and_wait<W>(p.base, mine, 0, par, me, b, gen, counters + k2Blocks);
+
+  // 2) reduce my chunk in rank order (fp32) and push the result to every rank's slot2
+  {
+    int64_t lo, hi;
+    span(me, lo, hi);
+    for (int64_t i = lo + 8 * threadIdx.x; i < hi; i += 8 * kThreads) {
+      const int cnt = i + 8 <= hi ? 8 : static_cast<int>(hi - i);
+      const int64_t o = off + (i - lo);  // element index inside a slot
+      float acc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        const uint16_t* src = slot2_ptr<W>(mine, 0, par, q, p.chunk_max) + o;
+        if (cnt == 8) {
+          const V v = *reinterpret_cast<const V*>(src);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += to_f32<T>(v.v[j]);
+        } else {
+          for (int j = 0; j < cnt; ++j) acc[j] += to_f32<T>(src[j]);
+        }
+      }
+      V r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r.v[j] = from_f32<T>(acc[j]);
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        uint16_t* dst = slot2_ptr<W>(p.base[q], 1, par, me, p.chunk_max) + o;
+        if (cnt == 8)
+          *reinterpret_cast<V*>(dst) = r;
+        else
+          for (int j = 0; j < cnt; ++j) dst[j] = r.v[j];
+      }
+    }
+  }
+  raise_and_wait<W>(p.base, mine, 1, par, me, b, gen, counters + k2Blocks);
+
+  // 3) gather every rank's reduced chunk (sub-range b) into y
+#pragma unroll
+  for (int q = 0; q < W; ++q) {
+    int64_t lo, hi;
+    span(q, lo, hi);
+    const uint16_t* src = slot2_ptr<W>(mine, 1, par, q, p.chunk_max) + off - lo;
+    for (int64_t i = lo + 8 * threadIdx.x; i < hi; i += 8 * kThreads) {
+      if (i + 8 <= hi)
+        *reinterpret_cast<V*>(y + i) = *reinterpret_cast<const V*>(src + i);
+      else
+        for (int64_t j = i; j < hi; ++j) y[j] = src[j];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) counters[b] = gen;
+}
+
+template <typename T>
+static int launch2(const Params2& p, const void* x, void* y, int64_t n, hipStream_t st) {
+  const uint16_t* xi = static_cast<const uint16_t*>(x);
+  uint16_t* yo = static_cast<uint16_t*>(y);
+  switch (p.world) {
+    case 2: twoshot_kernel<T, 2><<<k2Blocks, kThreads, 0, st>>>(p, xi, yo, n); break;
+    case 4: twoshot_kernel<T, 4><<<k2Blocks, kThreads, 0, st>>>(p, xi, yo, n); break;
+    case 8: twoshot_kernel<T, 8><<<k2Blocks, kThreads, 0, st>>>(p, xi, yo, n); break;
+    default: return -1;
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
 template <typename T>
 static int launch(const Params& p, const void* x, void* y, int64_t n, int blocks,
                   hipStream_t st) {
@@ -194,4 +363,34 @@ int atta_ar_run(void* const* bases, int rank, int world, int64_t max_elems, cons
   // fixed grid (see the generation argument above); blocks past the data only signal
   return dtype == 0 ? ar::launch<__bf16>(p, x, y, n, ar::kMaxBlocks, stream)
                     : ar::launch<_Float16>(p, x, y, n, ar::kMaxBlocks, stream);
+}
+
+// ---- two-shot entry points --------------------------------------------------------------
+static int64_t chunk_max_of(int64_t max_elems, int world) {
+  int64_t c = (max_elems + world - 1) / world;
+  c = (c + 7) & ~int64_t(7);
+  // + one sub-range of slack: the last block's sub-range may run past the chunk end
+  return c + ((c / ar::k2Blocks + 8) & ~int64_t(7));
+}
+
+size_t atta_ar2_buffer_bytes(int64_t max_elems, int world, int elem_bytes) {
+  return ar::k2HeaderBytes +
+         4 * static_cast<size_t>(world) * chunk_max_of(max_elems, world) * elem_bytes;
+}
+
+int64_t atta_ar2_error_offset() {
+  return static_cast<int64_t>((2 * ar::k2FlagWords + ar::k2Blocks) * sizeof(uint32_t));
+}
+
+int atta_ar2_run(void* const* bases, int rank, int world, int64_t max_elems, const void* x,
+                 void* y, int64_t n, int dtype, hipStream_t stream) {
+  if (world != 2 && world != 4 && world != 8) return -1;
+  if (rank < 0 || rank >= world || n <= 0 || n > max_elems) return -1;
+  ar::Params2 p{};
+  for (int i = 0; i < world; ++i) p.base[i] = static_cast<uint8_t*>(bases[i]);
+  p.rank = rank;
+  p.world = world;
+  p.chunk_max = chunk_max_of(max_elems, world);
+  return dtype == 0 ? ar::launch2<__bf16>(p, x, y, n, stream)
+                    : ar::launch2<_Float16>(p, x, y, n, stream);
 }

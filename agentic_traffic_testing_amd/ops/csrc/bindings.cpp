@@ -344,10 +344,12 @@ void fused_lm_head_sample(at::Tensor tokens, at::Tensor keys, const at::Tensor& 
 
 // Row-wise fp8 activation quantisation fused into norm / SiLU-mul / plain rows.
 void quant_rows_fp8(at::Tensor q, at::Tensor scale, const at::Tensor& x,
-                    const c10::optional<at::Tensor>& w, int64_t mode, double eps) {
+                    const c10::optional<at::Tensor>& w, int64_t mode, double eps,
+                    const c10::optional<at::Tensor>& residual) {
   check_dev(x, "x");
   check_dev(q, "q");
-  TORCH_CHECK(mode >= 0 && mode <= 2, "quant_rows_fp8: mode 0 (norm) / 1 (silu) / 2 (plain)");
+  TORCH_CHECK(mode >= 0 && mode <= 3,
+              "quant_rows_fp8: mode 0 (norm) / 1 (silu) / 2 (plain) / 3 (add + norm)");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && q.dim() == 2 && q.stride(1) == 1 &&
                   q.scalar_type() == at::kByte,
               "quant_rows_fp8: 2-D rows, uint8 q");
@@ -360,8 +362,19 @@ void quant_rows_fp8(at::Tensor q, at::Tensor scale, const at::Tensor& x,
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(q.data_ptr()) % 8 == 0,
               "quant_rows_fp8: 16-byte aligned x rows, 8-byte aligned q rows");
+  void* rp = nullptr;
+  int64_t rs = 0;
+  if (mode == 3) {
+    TORCH_CHECK(residual.has_value() && residual->sizes() == x.sizes() &&
+                    residual->stride(1) == 1 && residual->scalar_type() == x.scalar_type() &&
+                    residual->is_cuda() &&
+                    reinterpret_cast<uintptr_t>(residual->data_ptr()) % 16 == 0,
+                "quant_rows_fp8: mode 3 needs a residual shaped like x");
+    rp = residual->data_ptr();
+    rs = residual->stride(0);
+  }
   const void* wp = nullptr;
-  if (mode == 0) {
+  if (mode == 0 || mode == 3) {
     TORCH_CHECK(w.has_value() && w->numel() == width && w->scalar_type() == x.scalar_type() &&
                     w->is_cuda() && w->is_contiguous(),
                 "quant_rows_fp8: norm weight [width]");
@@ -370,7 +383,7 @@ void quant_rows_fp8(at::Tensor q, at::Tensor scale, const at::Tensor& x,
   const at::DeviceGuard g(x.device());
   check_rc(atta_quant_rows_fp8(q.data_ptr(), scale.data_ptr<float>(), x.data_ptr(), wp,
                                x.size(0), width, x.stride(0), q.stride(0), mode,
-                               static_cast<float>(eps), dtype_code(x), cur_stream()),
+                               static_cast<float>(eps), rp, rs, dtype_code(x), cur_stream()),
            "quant_rows_fp8");
 }
 
@@ -492,6 +505,33 @@ void ar_run(const at::Tensor& x, at::Tensor y, at::IntArrayRef bases, int64_t ra
            "ar_run");
 }
 
+int64_t ar2_buffer_bytes(int64_t max_elems, int64_t world, int64_t elem_bytes) {
+  return static_cast<int64_t>(
+      atta_ar2_buffer_bytes(max_elems, static_cast<int>(world), static_cast<int>(elem_bytes)));
+}
+
+int64_t ar2_error(int64_t ptr) {
+  uint32_t word = 0;
+  check_rc(static_cast<int>(hipMemcpy(&word, reinterpret_cast<uint8_t*>(ptr) + atta_ar2_error_offset(),
+                                      sizeof(word), hipMemcpyDeviceToHost)),
+           "ar2_error");
+  return word;
+}
+
+void ar2_run(const at::Tensor& x, at::Tensor y, at::IntArrayRef bases, int64_t rank,
+             int64_t max_elems) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel() &&
+                  x.scalar_type() == y.scalar_type(), "ar2_run: layout");
+  TORCH_CHECK(bases.size() >= 2 && bases.size() <= 8, "ar2_run: 2..8 ranks");
+  void* b[8] = {};
+  for (size_t i = 0; i < bases.size(); ++i) b[i] = reinterpret_cast<void*>(bases[i]);
+  const at::DeviceGuard g(x.device());
+  check_rc(atta_ar2_run(b, static_cast<int>(rank), static_cast<int>(bases.size()), max_elems,
+                        x.data_ptr(), y.data_ptr(), x.numel(), dtype_code(x), cur_stream()),
+           "ar2_run");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(atta, m) {
@@ -503,6 +543,9 @@ TORCH_LIBRARY(atta, m) {
   m.def("ar_close(int ptr) -> ()", &ar_close);
   m.def("ar_error(int ptr) -> int", &ar_error);
   m.def("ar_run(Tensor x, Tensor(a!) y, int[] bases, int rank, int max_elems) -> ()");
+  m.def("ar2_buffer_bytes(int max_elems, int world, int elem_bytes) -> int", &ar2_buffer_bytes);
+  m.def("ar2_error(int ptr) -> int", &ar2_error);
+  m.def("ar2_run(Tensor x, Tensor(a!) y, int[] bases, int rank, int max_elems) -> ()");
   m.def("skinny_variant(Tensor(a!) y, Tensor x, Tensor w, int variant) -> ()");
   m.def(
       "attention_decode_v2(Tensor(a!) out, Tensor(b!) part_out, Tensor(c!) part_lse, "
@@ -517,7 +560,7 @@ TORCH_LIBRARY(atta, m) {
         "bool preshuffled=False, Tensor? w_scale=None, int ksplit=1) -> ()");
   m.def("set_splitk_workspace(Tensor ws, Tensor counters) -> ()");
   m.def("quant_rows_fp8(Tensor(a!) q, Tensor(b!) scale, Tensor x, Tensor? w, int mode, "
-        "float eps) -> ()");
+        "float eps, Tensor(c!)? residual=None) -> ()");
   m.def(
       "fused_lm_head_sample(Tensor(a!) tokens, Tensor(b!) keys, Tensor x, Tensor w, float eps, "
       "Tensor temperature, Tensor seeds, Tensor steps, int finalize, int vocab_offset, "
@@ -551,6 +594,7 @@ TORCH_LIBRARY(atta, m) {
 
 TORCH_LIBRARY_IMPL(atta, CUDA, m) {
   m.impl("ar_run", &ar_run);
+  m.impl("ar2_run", &ar2_run);
   m.impl("rms_norm", &rms_norm);
   m.impl("fused_add_rms_norm", &fused_add_rms_norm);
   m.impl("silu_and_mul", &silu_and_mul);

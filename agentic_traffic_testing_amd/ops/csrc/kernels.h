@@ -89,11 +89,11 @@ int atta_skinny_variant(void* y, const void* x, const void* w, int M, int N, int
                         int variant, hipStream_t stream);
 
 // Row-wise e4m3fn activation quantisation (quant_fp8.hip): mode 0 = rmsnorm(x) * w,
-// 1 = silu(gate) * up (x rows hold gate | up, width = I), 2 = x.  q [rows, width] uint8,
-// scale [rows] fp32 (dequant: value = fp8 * scale).
+// 1 = silu(gate) * up (x rows hold gate | up, width = I), 2 = x, 3 = residual += x then
+// rmsnorm(residual) * w.  q [rows, width] uint8, scale [rows] fp32 (value = fp8 * scale).
 int atta_quant_rows_fp8(void* q, float* scale, const void* x, const void* w, int rows, int width,
-                        int64_t x_stride, int64_t q_stride, int mode, float eps, int dtype,
-                        hipStream_t stream);
+                        int64_t x_stride, int64_t q_stride, int mode, float eps, void* residual,
+                        int64_t res_stride, int dtype, hipStream_t stream);
 
 // ---- one-shot IPC all-reduce (allreduce.hip) ---------------------------------------------
 size_t atta_ar_buffer_bytes(int64_t max_elems, int elem_bytes);
@@ -106,3 +106,9 @@ int atta_ar_ipc_open(const void* handle, void** ptr);
 int atta_ar_ipc_close(void* ptr);
 int atta_ar_run(void* const* bases, int rank, int world, int64_t max_elems, const void* x,
                 void* y, int64_t n, int dtype, hipStream_t stream);
+
+// ---- two-shot IPC all-reduce (allreduce.hip): reduce-scatter + all-gather ----------------
+size_t atta_ar2_buffer_bytes(int64_t max_elems, int world, int elem_bytes);
+int64_t atta_ar2_error_offset();
+int atta_ar2_run(void* const* bases, int rank, int world, int64_t max_elems, const void* x,
+                 void* y, int64_t n, int dtype, hipStream_t stream);

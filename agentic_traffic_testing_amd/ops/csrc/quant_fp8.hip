@@ -7,6 +7,8 @@
 //   MODE_NORM : q, s <- quant(rmsnorm(x) * w)            (input / post-attention norms)
 //   MODE_SILU : q, s <- quant(silu(gate) * up)           (gate | up packed, width 2I)
 //   MODE_PLAIN: q, s <- quant(x)                          (attention output -> o_proj)
+//   MODE_ADDNORM: r <- r + x (residual stream, rounded to T, written back);
+//                 q, s <- quant(rmsnorm(r) * w)          (GEMM output + residual + norm)
 //
 // One 256-thread workgroup per row, two passes over the (L2-resident) row: pass 1 gathers
 // sum(x^2) (norm) and the row amax of the unscaled values, pass 2 recomputes each value,
@@ -20,7 +22,7 @@ namespace q8 {
 
 constexpr int kThreads = 256;
 constexpr float kFp8Max = 448.f;
-enum Mode { MODE_NORM = 0, MODE_SILU = 1, MODE_PLAIN = 2 };
+enum Mode { MODE_NORM = 0, MODE_SILU = 1, MODE_PLAIN = 2, MODE_ADDNORM = 3 };
 
 template <typename T, int MODE>
 __device__ __forceinline__ void load8(float (&v)[8], const uint16_t* x, const uint16_t* w,
@@ -35,7 +37,7 @@ __device__ __forceinline__ void load8(float (&v)[8], const uint16_t* x, const ui
       const float sg = to_f32<T>(from_f32<T>(g / (1.f + __expf(-g))));
       v[j] = sg * to_f32<T>(b.v[j]);
     }
-  } else if constexpr (MODE == MODE_NORM) {
+  } else if constexpr (MODE == MODE_NORM || MODE == MODE_ADDNORM) {
     const Pack8 ww = *reinterpret_cast<const Pack8*>(w + 8 * idx);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = to_f32<T>(a.v[j]) * to_f32<T>(ww.v[j]);
@@ -48,15 +50,29 @@ __device__ __forceinline__ void load8(float (&v)[8], const uint16_t* x, const ui
 template <typename T, int MODE>
 __global__ __launch_bounds__(kThreads) void quant_rows_kernel(
     uint8_t* __restrict__ q, float* __restrict__ scale, const uint16_t* __restrict__ x,
-    const uint16_t* __restrict__ w, int width, int64_t x_stride, int64_t q_stride, float eps) {
+    const uint16_t* __restrict__ w, int width, int64_t x_stride, int64_t q_stride, float eps,
+    uint16_t* __restrict__ residual, int64_t res_stride) {
   __shared__ float red[2][kThreads / kWave];
   const int64_t row = blockIdx.x;
   const uint16_t* xr = x + row * x_stride;
   const int nvec = width >> 3;
+  if constexpr (MODE == MODE_ADDNORM) {
+    // r <- r + x; every later read of this row is of r (each thread re-reads only the
+    // chunks it wrote itself: program order, no barrier needed)
+    uint16_t* rr = residual + row * res_stride;
+    for (int i = threadIdx.x; i < nvec; i += kThreads) {
+      const Pack8 a = *reinterpret_cast<const Pack8*>(xr + 8 * i);
+      Pack8 b = *reinterpret_cast<const Pack8*>(rr + 8 * i);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b.v[j] = from_f32<T>(to_f32<T>(a.v[j]) + to_f32<T>(b.v[j]));
+      *reinterpret_cast<Pack8*>(rr + 8 * i) = b;
+    }
+    xr = rr;
+  }
   float ss = 0.f, amax = 0.f;
   for (int i = threadIdx.x; i < nvec; i += kThreads) {
     float v[8];
-    if constexpr (MODE == MODE_NORM) {
+    if constexpr (MODE == MODE_NORM || MODE == MODE_ADDNORM) {
       const Pack8 a = *reinterpret_cast<const Pack8*>(xr + 8 * i);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -87,7 +103,9 @@ __global__ __launch_bounds__(kThreads) void quant_rows_kernel(
     ss += red[0][k];
     amax = fmaxf(amax, red[1][k]);
   }
-  const float inv_rms = MODE == MODE_NORM ? rsqrtf(ss / static_cast<float>(width) + eps) : 1.f;
+  const float inv_rms = (MODE == MODE_NORM || MODE == MODE_ADDNORM)
+                            ? rsqrtf(ss / static_cast<float>(width) + eps)
+                            : 1.f;
   amax *= inv_rms;
   const float s = amax > 0.f ? amax / kFp8Max : 1.f;
   const float rs = inv_rms / s;
@@ -111,20 +129,24 @@ __global__ __launch_bounds__(kThreads) void quant_rows_kernel(
 template <typename T>
 static int launch(int mode, uint8_t* q, float* scale, const uint16_t* x, const uint16_t* w,
                   int rows, int width, int64_t x_stride, int64_t q_stride, float eps,
-                  hipStream_t st) {
+                  uint16_t* res, int64_t res_stride, hipStream_t st) {
   const dim3 grid(rows), blk(kThreads);
   switch (mode) {
     case MODE_NORM:
       quant_rows_kernel<T, MODE_NORM><<<grid, blk, 0, st>>>(q, scale, x, w, width, x_stride,
-                                                            q_stride, eps);
+                                                            q_stride, eps, res, res_stride);
       return 0;
     case MODE_SILU:
       quant_rows_kernel<T, MODE_SILU><<<grid, blk, 0, st>>>(q, scale, x, w, width, x_stride,
-                                                            q_stride, eps);
+                                                            q_stride, eps, res, res_stride);
       return 0;
     case MODE_PLAIN:
       quant_rows_kernel<T, MODE_PLAIN><<<grid, blk, 0, st>>>(q, scale, x, w, width, x_stride,
-                                                             q_stride, eps);
+                                                             q_stride, eps, res, res_stride);
+      return 0;
+    case MODE_ADDNORM:
+      quant_rows_kernel<T, MODE_ADDNORM><<<grid, blk, 0, st>>>(q, scale, x, w, width, x_stride,
+                                                               q_stride, eps, res, res_stride);
       return 0;
     default:
       return -1;
@@ -137,17 +159,19 @@ static int launch(int mode, uint8_t* q, float* scale, const uint16_t* x, const u
 using namespace atta;
 
 int atta_quant_rows_fp8(void* q, float* scale, const void* x, const void* w, int rows, int width,
-                        int64_t x_stride, int64_t q_stride, int mode, float eps, int dtype,
-                        hipStream_t stream) {
+                        int64_t x_stride, int64_t q_stride, int mode, float eps, void* residual,
+                        int64_t res_stride, int dtype, hipStream_t stream) {
   if (width % 8 != 0 || x_stride % 8 != 0 || q_stride % 8 != 0) return -1;
-  if (mode == q8::MODE_NORM && w == nullptr) return -1;
+  if ((mode == q8::MODE_NORM || mode == q8::MODE_ADDNORM) && w == nullptr) return -1;
+  if (mode == q8::MODE_ADDNORM && (residual == nullptr || res_stride % 8 != 0)) return -1;
+  auto ro = static_cast<uint16_t*>(residual);
   if (rows == 0) return 0;
   auto qo = static_cast<uint8_t*>(q);
   auto xi = static_cast<const uint16_t*>(x);
   auto wi = static_cast<const uint16_t*>(w);
   const int rc = dtype == 0
-                     ? q8::launch<__bf16>(mode, qo, scale, xi, wi, rows, width, x_stride, q_stride, eps, stream)
-                     : q8::launch<_Float16>(mode, qo, scale, xi, wi, rows, width, x_stride, q_stride, eps, stream);
+                     ? q8::launch<__bf16>(mode, qo, scale, xi, wi, rows, width, x_stride, q_stride, eps, ro, res_stride, stream)
+                     : q8::launch<_Float16>(mode, qo, scale, xi, wi, rows, width, x_stride, q_stride, eps, ro, res_stride, stream);
   if (rc) return rc;
   return static_cast<int>(hipGetLastError());
 }

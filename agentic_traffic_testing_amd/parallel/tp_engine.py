@@ -96,13 +96,20 @@ def _backend(cfg: EngineConfig) -> str:
 
 
 def _maybe_ipc(cfg: EngineConfig, comm, runner: ModelRunner):
-    """Install the custom one-shot all-reduce for small (decode) messages when asked."""
-    if comm.size == 1 or not runner.is_cuda or cfg.tp_allreduce not in ("ipc",):
+    """Install the custom IPC all-reduce (one-shot for decode-sized messages, two-shot up to
+    a prefill chunk): always with tp_allreduce="ipc", and with "auto" when the ranks sit on
+    distinct GPUs of the node (RCCL backend) - the xGMI case it is built for."""
+    if comm.size == 1 or not runner.is_cuda or comm.size not in (2, 4, 8):
+        return
+    if cfg.tp_allreduce == "rccl":
+        return
+    if cfg.tp_allreduce == "auto" and (comm.is_gloo or cfg.tp_same_device):
         return
     from .custom_allreduce import IpcAllReduce
 
-    comm.ipc = IpcAllReduce(comm, runner.device,
-                            max_bytes=runner.max_seqs * runner.mcfg.hidden_size * 2)
+    H = runner.mcfg.hidden_size
+    comm.ipc = IpcAllReduce(comm, runner.device, max_bytes=runner.max_seqs * H * 2,
+                            large_max_bytes=min(cfg.max_num_batched_tokens, 8192) * H * 2)
 
 
 class TPEngine(LLMEngine):

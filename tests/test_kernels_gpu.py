@@ -545,7 +545,7 @@ def test_fp8_prefill_linear():
     assert float(err) < 0.08
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
 @pytest.mark.parametrize("m,width", [(1, 4096), (37, 8192), (300, 14336)])
 def test_quant_rows_fp8(mode, m, width):
     """Fused row-wise e4m3fn quantisation (norm / silu-mul / plain) vs the fp32 reference:
@@ -554,9 +554,13 @@ def test_quant_rows_fp8(mode, m, width):
     dt = torch.bfloat16
     x = torch.randn(m, 2 * width if mode == 1 else width, dtype=dt, device="cuda") * 3
     x[0] = 0 if mode == 2 else x[0]  # an all-zero row must not divide by zero
-    w = (1 + 0.1 * torch.randn(width, dtype=dt, device="cuda")) if mode == 0 else None
-    q, s = ops.quant_rows_fp8(x, mode, w, 1e-5)
-    qr, sr = ops.quant_rows_fp8(x.cpu(), mode, None if w is None else w.cpu(), 1e-5)
+    w = (1 + 0.1 * torch.randn(width, dtype=dt, device="cuda")) if mode in (0, 3) else None
+    res = torch.randn(m, width, dtype=dt, device="cuda") if mode == 3 else None
+    res_cpu = res.cpu() if res is not None else None
+    q, s = ops.quant_rows_fp8(x, mode, w, 1e-5, res)
+    qr, sr = ops.quant_rows_fp8(x.cpu(), mode, None if w is None else w.cpu(), 1e-5, res_cpu)
+    if mode == 3:  # residual stream updated in place, rounded like the bf16 add
+        assert torch.equal(res.cpu(), res_cpu)
     close(s.cpu(), sr, 0.0, 2e-2)
     deq = q.view(torch.float8_e4m3fn).float().cpu() * s.cpu()
     ref_v = qr.view(torch.float8_e4m3fn).float() * sr

@@ -259,19 +259,25 @@ def _ipc_ar_worker(rank, world, port, q):
 
         torch.cuda.set_device(0)
         comm = init_distributed(rank, world, "cuda:0", "gloo", "127.0.0.1", port)
-        ar = IpcAllReduce(comm, "cuda:0", max_bytes=16 * 8192 * 2)
+        ar = IpcAllReduce(comm, "cuda:0", max_bytes=16 * 8192 * 2,
+                          large_max_bytes=512 * 8192 * 2)
         bad = []
-        for it, n in enumerate([8, 7, 4096, 8192 * 5 + 3, 16 * 8192, 1000, 4096] * 6):
+        sizes = [8, 7, 4096, 8192 * 5 + 3, 16 * 8192, 1000, 4096, 300 * 8192 + 5, 512 * 8192]
+        for it, n in enumerate(sizes * 4):
             g = torch.Generator(device="cpu").manual_seed(1000 * it)
             parts = [torch.randn(n, generator=g).to(torch.bfloat16) for _ in range(world)]
             exp = torch.zeros(n)
-            for p_ in parts:  # rank order, fp32, like the kernel
+            for p_ in parts:  # rank order, fp32, like the kernels
                 exp += p_.float()
-            x = parts[rank].cuda()
-            ar.all_reduce(x)
-            torch.cuda.synchronize()
-            if not torch.equal(x.cpu(), exp.to(torch.bfloat16)):
-                bad.append((it, n))
+            exp = exp.to(torch.bfloat16)
+            # auto policy, then both kernels explicitly where the message fits them
+            modes = ["auto"] + (["oneshot"] if n <= ar.max_elems else []) + ["twoshot"]
+            for mode in modes:
+                x = parts[rank].cuda()
+                ar.all_reduce(x, mode)
+                torch.cuda.synchronize()
+                if not torch.equal(x.cpu(), exp):
+                    bad.append((it, n, mode))
         # graph-captured replays with fresh inputs each time
         x = torch.empty(4096, dtype=torch.bfloat16, device="cuda")
         s = torch.cuda.Stream()
@@ -281,15 +287,25 @@ def _ipc_ar_worker(rank, world, port, q):
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         graph = torch.cuda.CUDAGraph()
+        xl = torch.empty(200 * 8192, dtype=torch.bfloat16, device="cuda")
+        with torch.cuda.stream(s):
+            ar.all_reduce(xl.fill_(1.0), "twoshot")
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
         with torch.cuda.graph(graph):
             ar.all_reduce(x)
+            ar.all_reduce(xl, "twoshot")
         for k in range(5):
             x.fill_(float(rank + k))
+            xl.fill_(float(2 * rank - k))
             graph.replay()
             torch.cuda.synchronize()
             want = float(sum(r + k for r in range(world)))
             if not bool((x == want).all()):
                 bad.append(("graph", k, float(x[0])))
+            want2 = float(sum(2 * r - k for r in range(world)))
+            if not bool((xl == want2).all()):
+                bad.append(("graph2", k, float(xl[0])))
         if ar.check() != 0:
             bad.append(("timeout-word", ar.check()))
         comm.barrier()
@@ -302,11 +318,14 @@ def _ipc_ar_worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_ipc_allreduce_two_ranks_one_gpu():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_ipc_allreduce_ranks_one_gpu(world):
+    """One-shot and two-shot IPC all-reduce at 2 / 4 / 8 ranks (all on one MI355X): exact
+    fp32 rank-order sums for odd and prefill-sized messages, graph-captured replays."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    ps = [ctx.Process(target=_ipc_ar_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_ipc_ar_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
     res = sorted(q.get(timeout=300) for _ in ps)
@@ -314,4 +333,4 @@ def test_ipc_allreduce_two_ranks_one_gpu():
         p.join(timeout=60)
     for rank, bad, calls in res:
         assert bad == [], bad
-        assert calls > 40
+        assert calls > 20
