@@ -185,6 +185,31 @@ def build_runtime(force: bool = False) -> Path:
     return target
 
 
+SANITIZE_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+                  "-fno-sanitize-recover=undefined"]
+
+
+def sanitized_runtime_path() -> Path:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return RUNTIME_DIR / "_asan" / f"_atta_runtime{suffix}"
+
+
+def build_runtime_sanitized(force: bool = False) -> Path:
+    """ASan + UBSan build of the host runtime (block manager, step channel) for the CPU
+    sanitizer tier: same sources, own directory, loaded only by
+    tests/test_sanitizers.py under LD_PRELOAD=libasan (never by the serving stack)."""
+    target = sanitized_runtime_path()
+    target.parent.mkdir(parents=True, exist_ok=True)
+    srcs = sorted(RUNTIME_CSRC.glob("*.cpp"))
+    flags = [f for f in runtime_flags() if f != "-O3"]
+    cmd = ["g++", "-shared", *SANITIZE_FLAGS, *flags, *map(str, srcs), "-o", str(target)]
+    digest = _sha([*cmd, *_files_digest(runtime_sources())])
+    if force or not _stamp_ok(target, digest):
+        _run(cmd)
+        _write_stamp(target, digest)
+    return target
+
+
 def build_all(force: bool = False, jobs: int = 8, verbose: bool = False):
     rt = build_runtime(force=force)
     ks = build_kernels(force=force, jobs=jobs, verbose=verbose)

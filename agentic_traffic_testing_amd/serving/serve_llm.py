@@ -56,6 +56,9 @@ class Settings:
         self.metrics_prefix = e.get("LLM_METRICS_PREFIX", "llm")
         self.apply_template = _env_bool("LLM_APPLY_CHAT_TEMPLATE", "1")
         self.temperature = float(e.get("LLM_TEMPERATURE", "0.2"))
+        # benchmark knob: requests that do not say otherwise generate exactly max_tokens
+        # (bench/e2e.py; random-init weights would otherwise stop at random EOS draws)
+        self.ignore_eos = _env_bool("LLM_IGNORE_EOS", "")
         self.watchdog_s = float(e.get("LLM_WATCHDOG_SECONDS", "120"))
         # fault injection: exercise the agents' error / timeout paths
         self.fault_fail_rate = float(e.get("LLM_FAULT_FAIL_RATE") or "0")
@@ -223,7 +226,7 @@ async def handle_chat(request: web.Request) -> web.Response:
                f"prompt_len={len(original)}{tinfo}{trunc}")
 
         sp = SamplingParams(temperature=float(data.get("temperature", st.s.temperature)),
-                            max_tokens=max(1, eff_new), ignore_eos=bool(data.get("ignore_eos", False)),
+                            max_tokens=max(1, eff_new), ignore_eos=bool(data.get("ignore_eos", st.s.ignore_eos)),
                             seed=data.get("seed"))
         queue_wait = 0.0
         final = None

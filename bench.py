@@ -87,6 +87,10 @@ def parse_args(argv=None):
                     help="EngineConfig override for A/B runs (e.g. fuse_attn_oproj=0)")
     ap.add_argument("--parallel", choices=["dp", "tp"], default="dp",
                     help="dp: one engine replica per GPU (default); tp: one engine over all GPUs")
+    ap.add_argument("--via", choices=["engine", "http"], default="engine",
+                    help="engine: drive the engine in-process (headline); http: the whole "
+                         "serving stack - aiohttp llm-backend + Agent A + 5 Agent B over "
+                         "127.0.0.1, POST /task agentic_parallel (bench/e2e.py)")
     return ap.parse_args(argv)
 
 
@@ -184,6 +188,8 @@ def main_dp(a, world: int):
             print(*x, file=sys.stderr, flush=True)
 
     log(f"init {init_s:.1f}s kv_blocks={eng.runner.num_blocks} graphs={sorted(eng.runner.graphs)}")
+    if a.via == "http":
+        return _finish_http(a, eng, world, rank, dist, init_s, cfg, log)
     for i in range(a.warmup):
         r = wl.run_episode()
         log(f"warmup {i}: {r.completion_tokens / r.seconds:.1f} tok/s, {r.seconds:.2f}s")
@@ -262,6 +268,53 @@ def main_dp(a, world: int):
             "init_s": round(init_s, 1),
         }
         print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+def _finish_http(a, eng, world, rank, dist, init_s, cfg, log):
+    """--via http: the fan-out through the real serving stack on every rank."""
+    from agentic_traffic_testing_amd.bench.e2e import run_e2e
+
+    if dist:
+        dist.barrier()
+    _sync(a)
+    r = run_e2e(eng, a.steps, a.warmup, fanout=a.fanout, max_tokens=a.max_tokens, log=log)
+    _sync(a)
+    elapsed, tokens = r["seconds"], r["tokens"]
+    per_rank = [round(r["tokens_per_s"], 2)]
+    p50, p95 = r["p50_ttft_s"], r["p95_ttft_s"]
+    if dist:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (elapsed, tokens, p50, p95))
+        elapsed = max(g[0] for g in gathered)
+        tokens = sum(g[1] for g in gathered)
+        per_rank = [round(g[1] / g[0], 2) for g in gathered]
+        p50 = statistics.median(g[2] for g in gathered if g[2] is not None)
+        p95 = max(g[3] for g in gathered if g[3] is not None)
+    if rank == 0:
+        label = _model_label(a)
+        print(json.dumps({
+            "metric": METRIC, "value": round(tokens / elapsed, 2), "unit": "tokens/s",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1000.0, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if "bf" in a.dtype else a.dtype,
+            "weights": a.quantization or ("bf16" if "bf" in a.dtype else a.dtype),
+            "data": DATA.format(label), "via": "http",
+            "config": {"model": f"{label} (random-init)", "global_batch": a.fanout * world,
+                       "seq_len": a.max_model_len,
+                       "parallelism": f"dp{world}" if world > 1 else "tp1",
+                       "max_tokens": a.max_tokens, "hipgraphs": cfg.use_graphs,
+                       "stack": "aiohttp llm-backend + agent-a + 5 agent-b (127.0.0.1)",
+                       "device": a.device},
+            "per_rank_tokens_per_s": per_rank,
+            "p50_ttft_s": round(p50, 4) if p50 is not None else None,
+            "p95_ttft_s": round(p95, 4) if p95 is not None else None,
+            "llm_calls": r["calls"], "completion_tokens": int(tokens),
+            "per_task_s": r["per_task_s"], "init_s": round(init_s, 1)}), flush=True)
     if dist:
         dist.barrier()
         dist.destroy_process_group()

@@ -68,3 +68,14 @@ def test_bench_tp2_cpu():
     o = out[0]
     assert o["n_gpus"] == 2 and o["config"]["parallelism"] == "tp2"
     assert o["scaling"] == "strong" and o["completion_tokens"] == 7 * 4
+
+
+def test_bench_via_http_cpu():
+    """--via http: the fan-out through aiohttp llm-backend + Agent A + 5 Agent B; every LLM
+    call of each /task (planning, 5 workers, synthesis) generates exactly max_tokens."""
+    r, out = _run([*SMALL, "--via", "http"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    o = out[-1]
+    assert o["via"] == "http" and o["llm_calls"] == 7
+    assert o["completion_tokens"] == 7 * 4
+    assert o["p50_ttft_s"] is not None and o["p50_ttft_s"] > 0
