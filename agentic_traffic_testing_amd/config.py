@@ -83,6 +83,11 @@ MODEL_PRESETS: dict[str, ModelConfig] = {
     "small": ModelConfig(name="small", vocab_size=32768, hidden_size=1024, intermediate_size=2816,
                          num_layers=4, num_heads=8, num_kv_heads=2, max_position_embeddings=8192,
                          bos_token_id=32512, eos_token_ids=(32513, 32521)),
+    # long-context tests: the "small" shape with a 32k RoPE table (reference .env runs 11k)
+    "small-32k": ModelConfig(name="small-32k", vocab_size=32768, hidden_size=1024,
+                             intermediate_size=2816, num_layers=4, num_heads=8, num_kv_heads=2,
+                             max_position_embeddings=32768, bos_token_id=32512,
+                             eos_token_ids=(32513, 32521)),
     # TP rehearsal shape: 8 q heads over 2 KV heads, so TP=4/8 replicate KV heads (kv_rep > 1)
     "tiny-tp8": ModelConfig(name="tiny-tp8", vocab_size=4096, hidden_size=256,
                             intermediate_size=512, num_layers=2, num_heads=8, num_kv_heads=2,

@@ -15,6 +15,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from ..config import EngineConfig, resolve_model
+from ..utils import roctx
 from .model_runner import ModelRunner
 from .scheduler import Batch, Scheduler
 from .sequence import SamplingParams, Sequence, SeqStatus
@@ -135,18 +136,27 @@ class LLMEngine:
         with self.lock:
             if self._inflight is None:
                 ts = time.perf_counter()
-                batch = self.scheduler.schedule()
+                with roctx.range("engine.schedule"):
+                    batch = self.scheduler.schedule()
                 if batch.empty:
                     return []
                 t0 = time.perf_counter()
                 self.timing["schedule"] += t0 - ts
                 if not (self.cfg.async_decode and self.runner.launchable(batch)):
-                    return self._sync_step(batch, t0)
-                self._inflight = self._launch(batch, lookahead=False)
+                    with roctx.range("engine.sync_step" if batch.num_decode == len(batch.seqs)
+                                     else "engine.prefill_step"):
+                        return self._sync_step(batch, t0)
+                with roctx.range("engine.launch"):
+                    self._inflight = self._launch(batch, lookahead=False)
             cur = self._inflight
             nxt = self._lookahead_batch(cur)
-            self._inflight = self._launch(nxt, lookahead=True) if nxt is not None else None
-            return self._collect(cur)
+            if nxt is not None:
+                with roctx.range("engine.launch_lookahead"):
+                    self._inflight = self._launch(nxt, lookahead=True)
+            else:
+                self._inflight = None
+            with roctx.range("engine.collect"):
+                return self._collect(cur)
 
     def _launch(self, batch, lookahead: bool) -> "_Inflight":
         t0 = time.perf_counter()

@@ -262,6 +262,7 @@ async def handle_chat(request: web.Request) -> web.Response:
             ntok = len(final.token_ids) if final is not None else 0
             st.log(f"[llm] req={request_id} GENERATED tokens={ntok} time={el:.2f}s "
                    f"speed={ntok / el if el > 0 else 0:.1f} tok/s")
+            _engine_spans(st, wait_span, gen_span, final)
             if gen_span is not None:
                 gen_span.set_attribute("llm.generate_ms", int((time.monotonic() - t_first) * 1000))
                 gen_span.end()
@@ -303,6 +304,35 @@ async def handle_chat(request: web.Request) -> web.Response:
             "completion_tokens_text": st.tok.count(text),
         }
         return web.json_response({"output": text, "meta": meta})
+
+
+def _engine_spans(st: ServerState, wait_span, gen_span, final) -> None:
+    """Engine-side child spans, recorded from the request's engine timestamps: queueing +
+    prefill under ``llm.time_to_first_token`` (engine.prefill) and the decode steps under
+    ``llm.generate`` (engine.decode_step, one span carrying the step count)."""
+    if final is None or final.first_token_time is None:
+        return
+    off = time.time_ns() - time.perf_counter_ns()
+
+    def ns(t: float) -> int:
+        return int(t * 1e9) + off
+
+    sched = final.first_scheduled_time or final.arrival_time
+    sp = st.tracer.start_span("engine.prefill", context=otel.context_of(wait_span),
+                              start_time=ns(sched))
+    sp.set_attribute("llm.prompt_tokens", final.prompt_tokens)
+    sp.set_attribute("llm.cached_prompt_tokens", final.cached_prompt_tokens)
+    sp.set_attribute("engine.queue_ms", round((sched - final.arrival_time) * 1e3, 3))
+    sp.end(end_time=ns(final.first_token_time))
+    if gen_span is not None and final.finish_time is not None:
+        steps = max(0, len(final.token_ids) - 1)
+        dec = st.tracer.start_span("engine.decode_step", context=otel.context_of(gen_span),
+                                   start_time=ns(final.first_token_time))
+        dec.set_attribute("engine.decode_steps", steps)
+        if steps:
+            dec.set_attribute("engine.mean_step_ms",
+                              round((final.finish_time - final.first_token_time) * 1e3 / steps, 4))
+        dec.end(end_time=ns(final.finish_time))
 
 
 def create_app(state: ServerState) -> web.Application:

@@ -80,9 +80,9 @@ class Span:
     def is_recording(self) -> bool:
         return self.end_ns is None
 
-    def end(self):
+    def end(self, end_time: int | None = None):
         if self.end_ns is None:
-            self.end_ns = time.time_ns()
+            self.end_ns = time.time_ns() if end_time is None else int(end_time)
             if self._exporter is not None:
                 self._exporter.submit(self)
 
@@ -105,6 +105,11 @@ _current: contextvars.ContextVar[_Ctx] = contextvars.ContextVar("atta_otel_ctx",
 
 def get_current() -> _Ctx:
     return _current.get()
+
+
+def context_of(span: Span) -> _Ctx:
+    """A context whose current span is ``span`` (to parent a child without entering it)."""
+    return _Ctx(span=span)
 
 
 def attach(ctx: _Ctx):
@@ -241,9 +246,13 @@ class Tracer:
         return SpanContext(tid, self._rand.getrandbits(64) or 1, 1, False)
 
     def start_span(self, name: str, context: _Ctx | None = None,
-                   kind: SpanKind = SpanKind.INTERNAL, attributes: dict | None = None) -> Span:
+                   kind: SpanKind = SpanKind.INTERNAL, attributes: dict | None = None,
+                   start_time: int | None = None) -> Span:
+        """``start_time``: epoch ns (OTel API), for spans recorded after the fact."""
         parent = (context if context is not None else _current.get()).span_context()
         sp = Span(name, self._new_ctx(parent), parent, kind, self.service, _exporter())
+        if start_time is not None:
+            sp.start_ns = int(start_time)
         if attributes:
             sp.attributes.update(attributes)
         return sp

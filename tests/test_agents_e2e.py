@@ -140,3 +140,31 @@ def test_trace_propagation(stack):
     r = httpx.post(stack.llm.url + "/chat", json={"prompt": "trace me", "max_tokens": 2},
                    headers={"traceparent": tp}, timeout=60).json()
     assert r["meta"]["otel"]["trace_id"] == "0af7651916cd43dd8448eb211c80319c"
+
+
+def test_engine_child_spans(stack, monkeypatch):
+    """engine.prefill (under llm.time_to_first_token) and engine.decode_step (under
+    llm.generate) are emitted per request with the engine's own timestamps."""
+    from agentic_traffic_testing_amd.utils import otel
+
+    spans = []
+
+    class Sink:
+        def submit(self, sp):
+            spans.append(sp)
+
+    monkeypatch.setattr(otel, "_exporter", lambda: Sink())
+    tp = "00-1af7651916cd43dd8448eb211c80319c-b7ad6b7169203331-01"
+    r = httpx.post(stack.llm.url + "/chat", json={"prompt": "spans please", "max_tokens": 5},
+                   headers={"traceparent": tp}, timeout=60)
+    assert r.status_code == 200
+    by = {s.name: s for s in spans}
+    for name in ("llm.time_to_first_token", "llm.generate", "engine.prefill",
+                 "engine.decode_step"):
+        assert name in by, sorted(by)
+    pre, dec = by["engine.prefill"], by["engine.decode_step"]
+    assert pre.parent.span_id == by["llm.time_to_first_token"].get_span_context().span_id
+    assert dec.parent.span_id == by["llm.generate"].get_span_context().span_id
+    assert pre.get_span_context().trace_id == 0x1af7651916cd43dd8448eb211c80319c
+    assert pre.start_ns <= pre.end_ns <= dec.start_ns <= dec.end_ns
+    assert dec.attributes["engine.decode_steps"] == 4

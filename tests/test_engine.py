@@ -182,3 +182,22 @@ def test_70b_geometry_fused_decode(quant):
     outs, bad = _check(eng, _prompts(vocab=16000), n=8, tol_logit=0.25)
     assert bad <= 1
     assert eng.runner.graph_steps > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_len", [11000, 20000])
+def test_long_context_decode(max_len):
+    """max_model_len 11000 (reference infra/.env.example:129): a ~10.5k-token prompt through
+    the flash prefill (chunked at 4096 tokens) and the fused graph decode (43 split-K
+    partitions of 256 tokens, in-kernel combine); 20000 exceeds the 64-partition in-kernel
+    combine and takes the two-kernel split-K fallback.  Greedy tokens vs the dense oracle."""
+    cfg = EngineConfig(model="small-32k", device="cuda", max_model_len=max_len,
+                       num_kv_blocks=2048, max_num_batched_tokens=4096, max_num_seqs=4,
+                       graph_batch_sizes=(1, 2, 4))
+    eng = LLMEngine(cfg)
+    assert eng.runner.fused_decode == (max_len <= 16384)
+    rng = np.random.default_rng(11)
+    prompt = rng.integers(300, 30000, size=10500).tolist()
+    outs, bad = _check(eng, [prompt], n=6, tol_logit=0.25)
+    assert bad == 0 or bad == 1
+    assert len(outs[0].token_ids) == 6
