@@ -172,6 +172,9 @@ class EngineConfig:
     # Off (0): 128-token partitions won in the isolated microbenchmark but lost inside the
     # real decode step (13.8 vs 12.3 us, profiles/r1_profile_v6_preshuffled.txt)
     decode_partition_tokens_small: int = 0
+    # decode hipGraphs per partition bucket (attention grid sized to the step's longest
+    # context, not max_model_len); buckets above max_model_len's count are dropped
+    graph_parts_buckets: tuple = (1, 2, 4, 6, 8, 12, 16, 24, 32, 48, 64)
     decode_small_batch_max: int = 2
     # chunked prefill: max prompt tokens of one sequence per step (0 = max_num_batched_tokens)
     long_prefill_token_threshold: int = 0

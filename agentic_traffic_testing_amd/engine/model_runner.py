@@ -65,6 +65,8 @@ class MetaLayout:
         add("tile_qoff", NT)
         add("feed_prev", 1)     # 1: decode rows take the previous step's device samples
         add("temperature", S, torch.float32)
+        add("top_p", S, torch.float32)  # >= 1: off
+        add("top_k", S)                 # <= 0: off
         add("logits_idx", S, torch.int64)
         add("seeds", S, torch.int64)
         add("steps", S, torch.int64)
@@ -135,6 +137,13 @@ class ModelRunner:
         if self.max_parts_small > 64:  # in-kernel combine handles <= 64 partitions
             self.part_tokens_small, self.max_parts_small = self.part_tokens, self.max_parts
         alloc_parts = max(self.max_parts, self.max_parts_small)
+        # decode graphs are captured per (batch bucket, partition bucket): the attention grid
+        # is (seqs, kv heads, partitions) and every workgroup past a sequence's context still
+        # costs a dispatch and a round trip - a 32-partition grid (max_model_len 8192) over
+        # 3k-token contexts ran 2.6x the workgroups it needed
+        # (profiles/r2_fused_qkv_attn_experiment.txt: B=8 attention 21.9 us vs 10.8 at B=1)
+        self.parts_buckets = sorted({p for p in cfg.graph_parts_buckets if p < self.max_parts}
+                                    | {self.max_parts})
         self.tile_tokens = ops.prefill_tile_tokens(self.model.g)
         self.graph_sizes = sorted(b for b in cfg.graph_batch_sizes)
         if comm is not None and comm.size > 1 and comm.is_gloo:
@@ -195,8 +204,9 @@ class ModelRunner:
         # the fused decode attention combines <= 64 partitions in-kernel (<= 16k tokens at
         # 256-token partitions); longer contexts use the two-kernel split-K path
         self.fused_decode = bool(cfg.fused_decode) and self.max_parts <= 64
-        self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
-        self.graph_io: dict[int, dict] = {}
+        # keyed (batch bucket, partition bucket)
+        self.graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
+        self.graph_io: dict[tuple, dict] = {}
         self.graph_pool = None
         self.steps = 0
         self.graph_steps = 0
@@ -278,17 +288,21 @@ class ModelRunner:
         input_ids = np.zeros(T, dtype=np.int32)
         row = 0
         temps = np.zeros(S, dtype=np.float32)
+        top_p = np.ones(S, dtype=np.float32)
+        top_k = np.zeros(S, dtype=np.int32)
         seeds = np.zeros(S, dtype=np.int64)
         steps = np.zeros(S, dtype=np.int64)
         for i, (seq, s0, n) in enumerate(zip(batch.seqs, batch.q_start, batch.q_len)):
             input_ids[row:row + n] = seq.token_array()[s0:s0 + n]
             row += n
             temps[i] = seq.sampling.temperature
+            top_p[i] = seq.sampling.top_p
+            top_k[i] = seq.sampling.top_k
             seeds[i] = seq.seed
             steps[i] = len(seq.output_ids)
         arrays = dict(d)
-        arrays.update(input_ids=input_ids, temperature=temps, seeds=seeds, steps=steps,
-                      feed_prev=np.zeros(1, dtype=np.int32))
+        arrays.update(input_ids=input_ids, temperature=temps, top_p=top_p, top_k=top_k,
+                      seeds=seeds, steps=steps, feed_prev=np.zeros(1, dtype=np.int32))
         return lay, arrays
 
     @property
@@ -326,27 +340,40 @@ class ModelRunner:
                         tile_qoff=v["tile_qoff"], logits_idx=v["logits_idx"],
                         num_decode=num_decode, num_tiles=num_tiles)
 
-    def _forward_sample(self, v: dict, md: AttnMeta, num_parts: int, special_sampling=None):
+    def parts_bucket(self, max_kv: int) -> int:
+        """Smallest partition bucket covering a decode step whose longest context is max_kv."""
+        need = max(1, math.ceil(max_kv / self.part_tokens))
+        return next((p for p in self.parts_buckets if p >= need), self.max_parts)
+
+    def _forward_sample(self, v: dict, md: AttnMeta, num_parts: int, special: bool = False):
+        """One step's forward + sampling; ``special``: some row uses top-p / top-k (logits
+        are materialised and the top-k / top-p kernel samples every row)."""
         m = self.model
         T = v["input_ids"].shape[0]
-        if (self.fused_decode and special_sampling is None and md.num_tiles == 0
+        if (self.fused_decode and md.num_tiles == 0
                 and md.num_decode == T and m.decode_fusable(T)):
+            ws = self._ws_for(T)
+            if ws["part_tokens"] == self.part_tokens:
+                # grid over this step's partition bucket only (num_parts covers every row)
+                ws = {**ws, "max_parts": min(num_parts, self.max_parts)}
             return m.forward_decode(v["input_ids"], md, self.k_layers, self.v_layers,
-                                    self._ws_for(T), v["temperature"], v["seeds"], v["steps"],
-                                    prev_tokens=self.ws["tokens"], feed_prev=v["feed_prev"])
+                                    ws, v["temperature"], v["seeds"], v["steps"],
+                                    prev_tokens=self.ws["tokens"], feed_prev=v["feed_prev"],
+                                    top_p=v["top_p"] if special else None, top_k=v["top_k"])
         decode_only = md.num_tiles == 0 and md.num_decode == T
         hidden = m.forward(v["input_ids"], md, self.k_layers, self.v_layers, self.part_out,
                            self.part_lse, num_parts, self.part_tokens,
                            prev_tokens=self.ws["tokens"] if decode_only else None,
                            feed_prev=v["feed_prev"] if decode_only else None)
         last = hidden.index_select(0, v["logits_idx"])
-        if special_sampling is None and m.decode_fusable(last.shape[0]) and \
+        if not special and m.decode_fusable(last.shape[0]) and \
                 last.shape[0] <= self.max_seqs and m.hidden_fusable():
             # fused LM head + Gumbel-max sampler on the (already normalised) last rows
             return m.sample_rows(last, 0.0, v["temperature"], v["seeds"], v["steps"], self.ws)
         logits = m.compute_logits(last)
-        if special_sampling is not None:
-            return special_sampling(logits)
+        if special:
+            return ops.sample_topkp(logits, v["temperature"], v["top_p"], v["top_k"],
+                                    v["seeds"], v["steps"])
         return ops.sample(logits, v["temperature"], v["seeds"], v["steps"])
 
     # ------------------------------------------------------------------------------------
@@ -356,9 +383,11 @@ class ModelRunner:
         if not (self.is_cuda and self.cfg.use_graphs and batch.num_decode == n and n > 0
                 and self.graph_sizes and n <= self.graph_sizes[-1]):
             return 0
-        if any(s.sampling.top_p < 1.0 or s.sampling.top_k > 0 for s in batch.seqs):
-            return 0
         return next(b for b in self.graph_sizes if b >= n)
+
+    @staticmethod
+    def _special(batch: Batch) -> bool:
+        return any(s.sampling.top_p < 1.0 or s.sampling.top_k > 0 for s in batch.seqs)
 
     def execute(self, batch: Batch) -> np.ndarray:
         """Run one step; returns sampled token ids (one per sequence in batch order)."""
@@ -367,7 +396,7 @@ class ModelRunner:
         if bucket:
             return self.collect(self.launch(batch))
         self.steps += 1
-        special = any(s.sampling.top_p < 1.0 or s.sampling.top_k > 0 for s in batch.seqs)
+        special = self._special(batch)
         lay, arrays = self._prepare(batch)
         max_kv = int(arrays["seq_kvlen"][:batch.num_decode].max()) if batch.num_decode else 0
         num_parts = max(1, math.ceil(max_kv / self.part_tokens))
@@ -376,15 +405,14 @@ class ModelRunner:
                         0, int(special), n, lay.size, 0], dtype=np.int32)
         if self.publisher is not None:
             self.publisher.publish(np.concatenate([hdr, host]))
-        sampler = self._special_sampler(batch) if special else None
-        toks = self._run(hdr, sampler)
+        toks = self._run(hdr)
         return toks[:n].cpu().numpy()
 
     def launchable(self, batch: Batch) -> bool:
-        """Decode-only batches with plain sampling can be launched asynchronously."""
+        """Decode-only batches can be launched asynchronously (every sampler runs on the
+        device and leaves its tokens in ws["tokens"])."""
         n = len(batch.seqs)
-        return (0 < n <= self.max_seqs and batch.num_decode == n
-                and not any(s.sampling.top_p < 1.0 or s.sampling.top_k > 0 for s in batch.seqs))
+        return 0 < n <= self.max_seqs and batch.num_decode == n
 
     def launch(self, batch: Batch, lookahead: bool = False) -> dict:
         """Enqueue one decode-only step (graph replay when a bucket fits, else eager) and its
@@ -393,17 +421,19 @@ class ModelRunner:
         (``ws["tokens"]``, not yet seen by the host), so the host never waits between steps
         (async look-ahead decode)."""
         if not self.launchable(batch):
-            raise ValueError("launch() needs a decode-only batch with plain sampling")
+            raise ValueError("launch() needs a decode-only batch")
         n = len(batch.seqs)
         bucket = self.graph_bucket(batch)
-        if bucket and bucket not in self.graphs:
-            self.capture(bucket)
+        special = int(self._special(batch))
         self.steps += 1
         t0 = time.perf_counter()
         if bucket:
             lay, arrays = self._prepare(batch, pad_seqs=bucket, tiles=False)
-            assert lay.size == self.graph_io[bucket]["layout"].size
-            num_parts = self.max_parts
+            num_parts = self.parts_bucket(int(arrays["seq_kvlen"][:n].max()))
+            if (bucket, num_parts, special) not in self.graphs:
+                self.capture(bucket, num_parts, bool(special))
+                t0 = time.perf_counter()
+            assert lay.size == self.graph_io[(bucket, num_parts, special)]["layout"].size
         else:
             lay, arrays = self._prepare(batch, tiles=False)
             max_kv = int(arrays["seq_kvlen"][:n].max())
@@ -411,7 +441,7 @@ class ModelRunner:
         arrays["feed_prev"] = np.array([1 if lookahead else 0], dtype=np.int32)
         host = self._pack(lay, arrays)
         hdr = np.array([OP_STEP, lay.T, lay.S, lay.W, lay.NT, batch.num_decode, num_parts,
-                        bucket, 0, n, lay.size, 0], dtype=np.int32)
+                        bucket, special, n, lay.size, 0], dtype=np.int32)
         if self.publisher is not None:
             self.publisher.publish(np.concatenate([hdr, host]))
         t1 = time.perf_counter()
@@ -441,13 +471,14 @@ class ModelRunner:
         self._last_collect = now
         return self.tok_host[h["slot"]][:h["n"]].numpy().copy()
 
-    def _run(self, hdr, sampler=None, worker: bool = False):
+    def _run(self, hdr):
         """Execute one step from its header; the packed metadata is in ``meta_host``."""
         T, S, W, NT, num_decode, num_parts, bucket, special, n, size = (int(x) for x in hdr[1:11])
         if bucket:
-            io = self.graph_io[bucket]
+            key = (bucket, num_parts, special)
+            io = self.graph_io[key]
             self._h2d(io["dev"], size)
-            self.graphs[bucket].replay()
+            self.graphs[key].replay()
             self.graph_steps += 1
             return io["out"]
         lay = MetaLayout(T, S, W, NT)
@@ -455,11 +486,9 @@ class ModelRunner:
         self._h2d(dev, size)
         v = lay.views(dev)
         md = self._meta(v, num_decode, NT)
-        if special and worker:
-            # rank 0 samples (top-p / top-k); workers only join the logits all-gather
-            sampler = _discard_sampler
-        out = self._forward_sample(v, md, num_parts, sampler)
-        if not special and NT == 0 and num_decode == T and out is not None:
+        # every rank samples (deterministic kernels over all-gathered logits under TP)
+        out = self._forward_sample(v, md, num_parts, bool(special))
+        if NT == 0 and num_decode == T and out is not None:
             # every rank keeps the decode samples where a look-ahead step embeds them from
             dev_toks = self.ws["tokens"]
             if out.data_ptr() != dev_toks.data_ptr():
@@ -490,7 +519,7 @@ class ModelRunner:
             if op == OP_STOP:
                 return
             if op == OP_CAPTURE:
-                self.capture(int(hdr[1]))
+                self.capture(int(hdr[1]), int(hdr[2]) or None, bool(hdr[3]))
                 continue
             if op == OP_BARRIER:
                 if self.is_cuda:
@@ -501,7 +530,7 @@ class ModelRunner:
             # alternate pinned buffers: no stream sync per step, only an event wait on the
             # copy two steps back before its buffer is rewritten
             self._next_meta_host()[:size] = data[HDR_WORDS:HDR_WORDS + size]
-            self._run(hdr, worker=True)
+            self._run(hdr)
             self.steps += 1
 
     def barrier(self):
@@ -524,42 +553,15 @@ class ModelRunner:
             finally:
                 self.publisher.close()
 
-    def _special_sampler(self, batch: Batch):
-        params = [s.sampling for s in batch.seqs]
-        seqs = list(batch.seqs)
-
-        def fn(logits):
-            out = torch.empty(logits.shape[0], dtype=torch.long, device=logits.device)
-            for i, (p, seq) in enumerate(zip(params, seqs)):
-                row = logits[i].float()
-                if not p.temperature > 1e-5:
-                    out[i] = torch.argmax(row)
-                    continue
-                row = row / p.temperature
-                if p.top_k > 0:
-                    kth = torch.topk(row, min(p.top_k, row.numel())).values[-1]
-                    row = row.masked_fill(row < kth, float("-inf"))
-                probs = torch.softmax(row, -1)
-                if p.top_p < 1.0:
-                    sp, si = torch.sort(probs, descending=True)
-                    cum = torch.cumsum(sp, 0)
-                    keep = cum - sp < p.top_p
-                    mask = torch.zeros_like(probs, dtype=torch.bool)
-                    mask[si[keep]] = True
-                    probs = torch.where(mask, probs, torch.zeros_like(probs))
-                    probs = probs / probs.sum()
-                g = torch.Generator(device=logits.device)
-                g.manual_seed((seq.seed * 1000003 + len(seq.output_ids)) & 0x7FFFFFFFFFFFFFFF)
-                out[i] = torch.multinomial(probs, 1, generator=g)[0]
-            return out
-        return fn
-
     # ------------------------------------------------------------------------------------
-    def capture(self, bucket: int):
-        """Capture a decode step for `bucket` sequences into a hipGraph."""
+    def capture(self, bucket: int, parts: int | None = None, special: bool = False):
+        """Capture a decode step for `bucket` sequences whose contexts fit `parts` attention
+        partitions (default: max_model_len) into a hipGraph; ``special``: the top-k / top-p
+        sampler variant (logits materialised)."""
+        parts = parts or self.max_parts
         if self.publisher is not None:
             hdr = np.zeros(HDR_WORDS, dtype=np.int32)
-            hdr[0], hdr[1] = OP_CAPTURE, bucket
+            hdr[0], hdr[1], hdr[2], hdr[3] = OP_CAPTURE, bucket, parts, int(special)
             self.publisher.publish(hdr)
         lay = MetaLayout(bucket, bucket, self.bt_width, 0)
         dev = torch.zeros(lay.size, dtype=torch.int32, device=self.device)
@@ -569,35 +571,40 @@ class ModelRunner:
         v["slot_mapping"].fill_(-1)
         v["logits_idx"].copy_(torch.arange(bucket, dtype=torch.int64))
         md = self._meta(v, bucket, 0)
+        # a capture may come between look-ahead steps (a new partition bucket mid-generation):
+        # the warm-up passes sample into ws["tokens"], which still holds the in-flight step's
+        # tokens the next step embeds - keep them (stream-ordered copy and restore)
+        saved_tokens = self.ws["tokens"].clone()
         stream = torch.cuda.Stream(self.device)
         stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(stream):
             for _ in range(2):  # warm up (hipBLASLt heuristics, allocator)
-                self._forward_sample(v, md, self.max_parts)
+                self._forward_sample(v, md, parts, special)
         torch.cuda.current_stream(self.device).wait_stream(stream)
         g = torch.cuda.CUDAGraph()
         if self.graph_pool is None:
             self.graph_pool = torch.cuda.graph_pool_handle()
         with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
-            out = self._forward_sample(v, md, self.max_parts)
+            out = self._forward_sample(v, md, parts, special)
+        self.ws["tokens"].copy_(saved_tokens)
         torch.cuda.synchronize(self.device)
-        self.graphs[bucket] = g
-        self.graph_io[bucket] = {"layout": lay, "dev": dev, "out": out}
+        key = (bucket, parts, int(special))
+        self.graphs[key] = g
+        self.graph_io[key] = {"layout": lay, "dev": dev, "out": out}
 
-    def capture_all(self):
+    def capture_all(self, all_parts: bool = False):
+        """Capture every batch bucket at the full partition count (shorter-context partition
+        buckets are captured on first use, or here with ``all_parts``)."""
         if not (self.is_cuda and self.cfg.use_graphs):
             return
         for b in self.graph_sizes:
-            if b not in self.graphs:
-                self.capture(b)
+            for p in (self.parts_buckets if all_parts else [self.max_parts]):
+                if (b, p, 0) not in self.graphs:
+                    self.capture(b, p)
 
     def reset_state(self):
         """Drop prefix cache contents (used between benchmark phases)."""
         self.bm.reset_prefix_cache()
-
-
-def _discard_sampler(logits):
-    return None
 
 
 __all__ = ["ModelRunner", "MetaLayout", "ref", "HDR_WORDS", "OP_STEP", "OP_CAPTURE", "OP_STOP",

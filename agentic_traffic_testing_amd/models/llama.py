@@ -368,13 +368,15 @@ class LlamaModel:
 
     def forward_decode(self, input_ids: torch.Tensor, md: AttnMeta, k_caches, v_caches, ws: dict,
                        temperature, seeds, steps, prev_tokens=None,
-                       feed_prev=None) -> torch.Tensor:
+                       feed_prev=None, top_p=None, top_k=None) -> torch.Tensor:
         """Fused decode step (every sequence has one query token); returns sampled ids.
 
         Per layer: [RMSNorm+QKV+RoPE+KV-write] -> [paged attention, in-kernel split-K
         combine] -> [o_proj + residual add] -> [RMSNorm+gate_up+SiLU*up] ->
         [down_proj + residual add]; then [final RMSNorm + LM head + sampler].  5 kernels per
-        layer instead of ~10, no normalised activations or logits ever hit HBM."""
+        layer instead of ~10, no normalised activations or logits ever hit HBM.  With
+        ``top_p`` / ``top_k`` (per-row device tensors) the step ends in final RMSNorm + LM head
+        + the top-k / top-p sampler kernel instead (logits materialised)."""
         eps = self.cfg.rms_norm_eps
         nq, nkv = self.n_heads, self.n_kv_heads
         B = input_ids.shape[0]
@@ -426,6 +428,10 @@ class LlamaModel:
                 residual.add_(self._all_reduce(ops.linear(act, L.down_ps if ps else L.down,
                                                           preshuffled=ps, w_scale=L.down_s,
                                                           ksplit=None, proj="down")))
+        if top_p is not None:
+            logits = self.compute_logits(ops.rms_norm(residual, self.norm, eps))
+            return ops.sample_topkp(logits, temperature, top_p, top_k, seeds, steps,
+                                    out=ws["tokens"][:B])
         return self.sample_rows(residual, eps, temperature, seeds, steps, ws)
 
     def sample_rows(self, x, eps, temperature, seeds, steps, ws) -> torch.Tensor:

@@ -198,6 +198,22 @@ def attention_decode(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, s
     return out
 
 
+def sample_topkp(logits, temperature, top_p, top_k, seeds, steps, out=None):
+    """top-k / top-p sampling, one workgroup per row (ops/csrc/sampling.hip): exact radix-select
+    thresholds, the same seeded Gumbel draw as ``sample`` (rows with both filters off get the
+    same token), device-side parameters - graph-capturable."""
+    if not logits.is_cuda:
+        r = ref.sample_topkp(logits, temperature, top_p, top_k, seeds, steps)
+        if out is not None:
+            out[:r.shape[0]].copy_(r)
+            return out[:r.shape[0]]
+        return r
+    if out is None:
+        out = torch.empty(logits.shape[0], dtype=torch.long, device=logits.device)
+    _native().sample_topkp(out, logits, temperature, top_p, top_k, seeds, steps)
+    return out[:logits.shape[0]]
+
+
 def sample(logits, temperature, seeds, steps, out=None):
     if not logits.is_cuda:
         r = ref.sample(logits, temperature, seeds, steps)
@@ -496,17 +512,19 @@ def fused_qkv_attention_ok(x, w, n_q_heads, n_kv_heads, k_cache, max_parts, pres
 
 def decode_qkv_attention(x, w, eps, positions, slots, cos_sin, k_cache, v_cache, n_q_heads,
                          n_kv_heads, block_tables, seq_kvlen, scale, ws, q_out, attn_out,
-                         w_scale=None):
+                         w_scale=None, wg_trace=None):
     """RMSNorm(x) -> QKV GEMV -> RoPE -> paged KV write AND the decode attention of the same
     rows in ONE launch (ops/csrc/attention_decode.hip qkv_attn_kernel): the attention
     workgroups load the cached context while the qkv workgroups stream the weights, then take
     q and the new token's k / v straight from them.  ``ws`` holds the split-K partials and the
-    hand-off words (ModelRunner.ws); 256-token partitions, ``ws["max_parts"]`` of them."""
+    hand-off words (ModelRunner.ws); 256-token partitions, ``ws["max_parts"]`` of them.
+    ``wg_trace`` (int64 [4 * workgroups]): per-workgroup [start, past-wait, end, CU id]
+    timeline on the 100 MHz wall clock (scripts/gpu/trace_fused_qkv_attn.py)."""
     _native().fused_qkv_attn(q_out, k_cache, v_cache, x, w, positions, slots, cos_sin, n_q_heads,
                              n_kv_heads, eps, attn_out, ws["part_out"], ws["part_lse"],
                              ws["counters"], block_tables, seq_kvlen, ws["max_parts"], scale,
                              ws["side_kv"], ws["pub_counters"], ws["exit_counters"],
-                             ws["fused_error"], w_scale)
+                             ws["fused_error"], w_scale, wg_trace)
     return attn_out
 
 

@@ -21,6 +21,9 @@
 #include "kernels.h"
 #include "skinny.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace atta {
 namespace dec {
 
@@ -74,6 +77,9 @@ struct DecParams {
   int* exit_counters;
   int pub_target, wgs_per_hk;
   int* error_word;          // bit 0: a wait timed out (results are garbage, host raises)
+  // optional per-workgroup timeline (100 MHz wall clock): [start, past-wait, end, hw id]
+  unsigned long long* wg_trace;
+  int poll_sleeps;          // consumer poll interval, ~0.27 us units (ATTA_FUSED_POLL_SLEEPS)
 };
 
 template <typename T>
@@ -83,12 +89,12 @@ struct TileFrags {
 };
 
 // Device-scope relaxed poll of one counter (one lane), bounded: ~1 s, then the error word.
-__device__ __forceinline__ void wait_count(int* ctr, int target, int* err) {
+__device__ __forceinline__ void wait_count(int* ctr, int target, int* err, int sleeps = 1) {
   uint32_t spins = 0;
-  // sparse polls (~0.3 us apart): pollers hammering the counter lines slow the weight
-  // stream of the producers they wait for (MI355X_MICROARCH.md polling-cost)
+  // sparse polls (sleeps x ~0.27 us apart): pollers hammering the counter lines slow the
+  // weight stream of the producers they wait for (MI355X_MICROARCH.md polling-cost)
   while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-    __builtin_amdgcn_s_sleep(10);
+    for (int i = 0; i < sleeps; ++i) __builtin_amdgcn_s_sleep(10);
     if (++spins > (1u << 20)) {
       __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
@@ -115,7 +121,9 @@ __device__ __forceinline__ void fused_exit(const DecParams& p, int hk) {
 
 template <typename T, int G, int WAVES, int TPW, bool FUSED>
 __device__ __forceinline__ void decode_attention_body(const DecParams& p, const int s,
-                                                      const int hk, const int part) {
+                                                      const int hk, const int part,
+                                                      unsigned long long& t_start,
+                                                      unsigned long long& t_wait) {
   using frag8 = typename Mf<T>::frag8;
   __shared__ float lds_o[WAVES][G][kD + 4];
   __shared__ float lds_m[WAVES][G];
@@ -146,6 +154,9 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
   asm volatile("" : "+s"(kvlen), "+s"(qrow));
 #pragma unroll
   for (int i = 0; i < TPW; ++i) asm volatile("" : "+s"(bte[i]));
+  // timeline probe (fused launch): clock reads only after the scalar loads above - an
+  // earlier one makes them vector loads, which the scalar-operand asm cannot take
+  if constexpr (FUSED) t_start = wall_clock64();
   const int nparts = (kvlen + PT - 1) / PT;
   if (part >= nparts) {  // block-uniform (also kvlen == 0 dummy sequences)
     if constexpr (FUSED) fused_exit(p, hk);
@@ -191,8 +202,9 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
   TileFrags<T> fn;  // fused: the newest token as a one-row tile (wave 0 of new_part)
   if constexpr (FUSED) {
     // the cache tiles above are in flight; now wait for this KV head's q / k / v producers
-    if (threadIdx.x == 0) wait_count(p.pub_counters + hk, p.pub_target, p.error_word);
+    if (threadIdx.x == 0) wait_count(p.pub_counters + hk, p.pub_target, p.error_word, p.poll_sleeps);
     __syncthreads();
+    t_wait = wall_clock64();  // timeline probe (stored at exit)
     // device-scope loads of the handed-off rows (written 16 B write-through by producers)
     const bool ok = col < G;
     const auto rq = dev_rsrc(p.q);
@@ -392,7 +404,9 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
 
 template <typename T, int G, int WAVES, int TPW>
 __global__ __launch_bounds__(WAVES * 64) void decode_attention_kernel(DecParams p) {
-  decode_attention_body<T, G, WAVES, TPW, false>(p, blockIdx.x, blockIdx.y, blockIdx.z);
+  unsigned long long t_start, t_wait;
+  decode_attention_body<T, G, WAVES, TPW, false>(p, blockIdx.x, blockIdx.y, blockIdx.z, t_start,
+                                                 t_wait);
 }
 
 template <typename T, int WAVES, int TPW>
@@ -433,15 +447,25 @@ template <typename T, int G, int MT, bool W8>
 __global__ __launch_bounds__(256) void qkv_attn_kernel(SkinnyParams sp, DecParams dp,
                                                        int n_tiles, int att_parts) {
   const int b = blockIdx.x;
+  // timeline probe: every store at the exit - a store ahead of the bodies' loads would let
+  // them alias it and demote their scalar loads to vector ones
+  unsigned long long t0 = 0, t_wait = 0;
   if (b < n_tiles) {
+    t0 = wall_clock64();
     skinny_body<T, 4, W8 ? 8 : 4, MT, EPI_QKVPUB, true, true, W8>(sp, b, 0);
-    return;
+  } else {
+    const int a = b - n_tiles;
+    const int part = a % att_parts;
+    const int hk = (a / att_parts) % dp.n_kv_heads;
+    const int s = a / (att_parts * dp.n_kv_heads);
+    decode_attention_body<T, G, 4, 4, true>(dp, s, hk, part, t0, t_wait);
   }
-  const int a = b - n_tiles;
-  const int part = a % att_parts;
-  const int hk = (a / att_parts) % dp.n_kv_heads;
-  const int s = a / (att_parts * dp.n_kv_heads);
-  decode_attention_body<T, G, 4, 4, true>(dp, s, hk, part);
+  if (dp.wg_trace != nullptr && threadIdx.x == 0) {
+    dp.wg_trace[4 * b] = t0;
+    dp.wg_trace[4 * b + 1] = t_wait;
+    dp.wg_trace[4 * b + 2] = wall_clock64();
+    dp.wg_trace[4 * b + 3] = __smid();
+  }
 }
 
 template <typename T, int MT, bool W8>
@@ -517,7 +541,7 @@ int atta_fused_qkv_attn(void* q_out, void* k_cache, void* v_cache, const void* x
                         float* part_lse, int* counters, const int* block_tables,
                         const int* seq_kvlen, int max_parts, int bt_stride, float scale,
                         void* side_kv, int* pub_counters, int* exit_counters, int* error_word,
-                        int dtype, hipStream_t stream) {
+                        unsigned long long* wg_trace, int dtype, hipStream_t stream) {
   const int G = n_q_heads / n_kv_heads;
   int shift = 0;
   while ((1 << shift) < block_size) ++shift;
@@ -574,6 +598,12 @@ int atta_fused_qkv_attn(void* q_out, void* k_cache, void* v_cache, const void* x
   dp.pub_target = G * 8 + 16;
   dp.wgs_per_hk = M * max_parts;
   dp.error_word = error_word;
+  dp.wg_trace = wg_trace;
+  static const int poll_sleeps = [] {
+    const char* e = getenv("ATTA_FUSED_POLL_SLEEPS");
+    return e ? std::max(1, atoi(e)) : 1;
+  }();
+  dp.poll_sleeps = poll_sleeps;
   const int n_tiles = sp.N / 16;
   dim3 grid(n_tiles + M * n_kv_heads * max_parts);
   const int mt = M <= 16 ? 1 : 2;

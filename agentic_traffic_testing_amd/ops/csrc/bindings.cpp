@@ -222,6 +222,29 @@ void sample(at::Tensor out, const at::Tensor& logits, const at::Tensor& temperat
            "sample");
 }
 
+void sample_topkp(at::Tensor out, const at::Tensor& logits, const at::Tensor& temperature,
+                  const at::Tensor& top_p, const at::Tensor& top_k, const at::Tensor& seeds,
+                  const at::Tensor& steps) {
+  check_dev(logits, "logits");
+  TORCH_CHECK(out.scalar_type() == at::kLong && seeds.scalar_type() == at::kLong &&
+                  steps.scalar_type() == at::kLong && temperature.scalar_type() == at::kFloat &&
+                  top_p.scalar_type() == at::kFloat && top_k.scalar_type() == at::kInt,
+              "sample_topkp: dtypes");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "sample_topkp: logits 2-D");
+  const int64_t rows = logits.size(0);
+  TORCH_CHECK(out.numel() >= rows && temperature.numel() >= rows && top_p.numel() >= rows &&
+                  top_k.numel() >= rows && seeds.numel() >= rows && steps.numel() >= rows,
+              "sample_topkp: per-row arrays");
+  const bool is_f32 = logits.scalar_type() == at::kFloat;
+  TORCH_CHECK(is_f32 || logits.scalar_type() == at::kBFloat16, "sample_topkp: logits fp32/bf16");
+  const at::DeviceGuard g(logits.device());
+  check_rc(atta_sample_topkp(out.data_ptr<int64_t>(), logits.data_ptr(), rows, logits.size(1),
+                             logits.stride(0), is_f32 ? 1 : 0, temperature.data_ptr<float>(),
+                             top_p.data_ptr<float>(), top_k.data_ptr<int>(),
+                             seeds.data_ptr<int64_t>(), steps.data_ptr<int64_t>(), cur_stream()),
+           "sample_topkp");
+}
+
 // fp8 weight-only quantisation: w is uint8 (OCP e4m3fn bytes, pre-shuffled in 16 x 64 blocks)
 // and w_scale the fp32 per-row dequant scale; returns the scale pointer (nullptr: 16-bit w).
 const float* fp8_scale(const at::Tensor& w, const c10::optional<at::Tensor>& w_scale,
@@ -446,7 +469,8 @@ void fused_qkv_attn(at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache, co
                     const at::Tensor& block_tables, const at::Tensor& seq_kvlen, int64_t max_parts,
                     double scale, at::Tensor side_kv, at::Tensor pub_counters,
                     at::Tensor exit_counters, at::Tensor error_word,
-                    const c10::optional<at::Tensor>& w_scale) {
+                    const c10::optional<at::Tensor>& w_scale,
+                    const c10::optional<at::Tensor>& wg_trace) {
   check_skinny(x, w, "fused_qkv_attn");
   const float* ws = fp8_scale(w, w_scale, "fused_qkv_attn");
   const int64_t M = x.size(0);
@@ -473,6 +497,14 @@ void fused_qkv_attn(at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache, co
   TORCH_CHECK(part_out.numel() >= M * n_kv_heads * max_parts * 16 * 128 &&
                   part_lse.numel() >= M * n_kv_heads * max_parts * 16,
               "fused_qkv_attn: split-K workspace");
+  unsigned long long* trace_ptr = nullptr;
+  if (wg_trace.has_value()) {
+    const int64_t wgs = (n_q_heads + 2 * n_kv_heads) * 8 + M * n_kv_heads * max_parts;
+    TORCH_CHECK(wg_trace->scalar_type() == at::kLong && wg_trace->is_contiguous() &&
+                    wg_trace->numel() >= 4 * wgs,
+                "fused_qkv_attn: wg_trace int64 [", 4 * wgs, "]");
+    trace_ptr = reinterpret_cast<unsigned long long*>(wg_trace->data_ptr<int64_t>());
+  }
   const at::DeviceGuard g(x.device());
   check_rc(atta_fused_qkv_attn(
                q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), x.data_ptr(), w.data_ptr(),
@@ -482,7 +514,7 @@ void fused_qkv_attn(at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache, co
                part_lse.data_ptr<float>(), counters.data_ptr<int>(), block_tables.data_ptr<int>(),
                seq_kvlen.data_ptr<int>(), max_parts, block_tables.stride(0),
                static_cast<float>(scale), side_kv.data_ptr(), pub_counters.data_ptr<int>(),
-               exit_counters.data_ptr<int>(), error_word.data_ptr<int>(), dtype_code(x),
+               exit_counters.data_ptr<int>(), error_word.data_ptr<int>(), trace_ptr, dtype_code(x),
                cur_stream()),
            "fused_qkv_attn");
 }
@@ -613,7 +645,7 @@ TORCH_LIBRARY(atta, m) {
       "float eps, Tensor(d!) out, Tensor(e!) part_out, Tensor(f!) part_lse, Tensor(g!) counters, "
       "Tensor block_tables, Tensor seq_kvlen, int max_parts, float scale, Tensor(h!) side_kv, "
       "Tensor(i!) pub_counters, Tensor(j!) exit_counters, Tensor(k!) error_word, "
-      "Tensor? w_scale=None) -> ()");
+      "Tensor? w_scale=None, Tensor(l!)? wg_trace=None) -> ()");
   m.def("quant_rows_fp8(Tensor(a!) q, Tensor(b!) scale, Tensor x, Tensor? w, int mode, "
         "float eps, Tensor(c!)? residual=None) -> ()");
   m.def(
@@ -645,6 +677,8 @@ TORCH_LIBRARY(atta, m) {
       "Tensor seq_qstart, int num_seqs, int num_parts, int part_tokens, int n_q_heads, int n_kv_heads, "
       "float scale) -> ()");
   m.def("sample(Tensor(a!) out, Tensor logits, Tensor temperature, Tensor seeds, Tensor steps) -> ()");
+  m.def("sample_topkp(Tensor(a!) out, Tensor logits, Tensor temperature, Tensor top_p, "
+        "Tensor top_k, Tensor seeds, Tensor steps) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(atta, CUDA, m) {
@@ -659,6 +693,7 @@ TORCH_LIBRARY_IMPL(atta, CUDA, m) {
   m.impl("flash_prefill", &flash_prefill);
   m.impl("attention_decode", &attention_decode);
   m.impl("sample", &sample);
+  m.impl("sample_topkp", &sample_topkp);
   m.impl("skinny_gemm", &skinny_gemm);
   m.impl("fused_qkv_rope", &fused_qkv_rope);
   m.impl("fused_gate_up_silu", &fused_gate_up_silu);

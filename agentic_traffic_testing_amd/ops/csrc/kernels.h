@@ -51,6 +51,12 @@ int atta_sample(int64_t* out, const void* logits, int rows, int vocab, int64_t s
                 int logits_is_fp32, const float* temperature, const int64_t* seeds,
                 const int64_t* steps, hipStream_t stream);
 
+// top-k / top-p sampling (exact radix-select thresholds, same Gumbel draw as atta_sample)
+int atta_sample_topkp(int64_t* out, const void* logits, int rows, int vocab, int64_t stride,
+                      int logits_is_fp32, const float* temperature, const float* top_p,
+                      const int* top_k, const int64_t* seeds, const int64_t* steps,
+                      hipStream_t stream);
+
 int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual, int M, int N,
                      int K, int64_t x_stride, int64_t y_stride, int64_t res_stride, int waves,
                      int ksplit, const float* wscale, int dtype, hipStream_t stream);
@@ -122,4 +128,4 @@ int atta_fused_qkv_attn(void* q_out, void* k_cache, void* v_cache, const void* x
                         float* part_lse, int* counters, const int* block_tables,
                         const int* seq_kvlen, int max_parts, int bt_stride, float scale,
                         void* side_kv, int* pub_counters, int* exit_counters, int* error_word,
-                        int dtype, hipStream_t stream);
+                        unsigned long long* wg_trace, int dtype, hipStream_t stream);

@@ -133,6 +133,45 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, seeds: torch.Tensor,
     return out
 
 
+def sample_topkp(logits: torch.Tensor, temperature, top_p, top_k, seeds,
+                 steps) -> torch.Tensor:
+    """top-k / top-p sampling with the kernel's definition (ops/csrc/sampling.hip): x =
+    logit * (1/T) in fp32; keep x >= the k-th largest x (top_k in (0, vocab)); then keep x >=
+    thr_p, the value at which the descending cumulative mass (32.32 fixed-point e^(x - max)
+    over the kept set) first reaches ceil(p * Z) (top_p < 1); argmax of x + Gumbel over the
+    kept set (lowest index on ties).  Greedy rows (T <= 1e-5) take argmax(logit)."""
+    lf = logits.float().cpu()
+    out = torch.empty(lf.shape[0], dtype=torch.long)
+    V = lf.shape[1]
+    for r in range(lf.shape[0]):
+        t = float(temperature[r])
+        if not t > 1e-5:
+            out[r] = int(torch.argmax(lf[r]))
+            continue
+        inv_t = torch.tensor(1.0, dtype=torch.float32) / torch.tensor(t, dtype=torch.float32)
+        x = lf[r] * inv_t
+        keep = torch.ones(V, dtype=torch.bool)
+        k = int(top_k[r])
+        if 0 < k < V:
+            keep &= x >= torch.topk(x, k).values[-1]
+        p = float(top_p[r])
+        if p < 1.0:
+            w = torch.where(keep, torch.floor((torch.exp(x - x.max()).double()) * 2.0 ** 32),
+                            torch.zeros((), dtype=torch.float64)).long()
+            z = int(w.sum())
+            target = max(1, math.ceil(float(torch.tensor(p, dtype=torch.float32)) * z))
+            xs, order = torch.sort(torch.where(keep, x, torch.tensor(float("-inf"))),
+                                   descending=True, stable=True)
+            cum = torch.cumsum(w[order], 0)
+            j = int(torch.nonzero(cum >= target)[0, 0])
+            keep &= x >= xs[j]
+        idx = torch.arange(V, dtype=torch.int64)
+        sc = x + gumbel_noise(int(seeds[r]), int(steps[r]), idx)
+        sc = torch.where(keep, sc, torch.tensor(float("-inf")))
+        out[r] = int(torch.argmax(sc))
+    return out.to(logits.device)
+
+
 def _ordered_bits(v: float) -> int:
     import struct
 

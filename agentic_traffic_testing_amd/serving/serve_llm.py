@@ -389,7 +389,7 @@ def build_engine(args):
         external = int(os.environ.get("WORLD_SIZE", "1")) == cfg.tensor_parallel_size
         return TPEngine(cfg, external=external)
     eng = LLMEngine(cfg)
-    eng.runner.capture_all()
+    eng.runner.capture_all(all_parts=True)
     return eng
 
 

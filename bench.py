@@ -179,7 +179,7 @@ def main_dp(a, world: int):
     cfg = _cfg(a, dev)
     t0 = time.perf_counter()
     eng = LLMEngine(cfg)
-    eng.runner.capture_all()
+    eng.runner.capture_all(all_parts=True)
     init_s = time.perf_counter() - t0
     wl = FanoutWorkload(eng, fanout=a.fanout, max_tokens=a.max_tokens, seed=rank)
 

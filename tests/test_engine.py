@@ -92,6 +92,119 @@ def test_graph_replay_equals_eager():
     assert res[0] == res[1]
 
 
+def test_parts_buckets_cover_context():
+    """Decode graphs are keyed by partition bucket: the bucket always covers the step's
+    longest context (every partition gets a workgroup) and never exceeds max_model_len's."""
+    cfg = EngineConfig(model="tiny", device="cpu", max_model_len=3000, num_kv_blocks=64)
+    r = LLMEngine(cfg).runner
+    assert r.max_parts == 12 and r.parts_buckets == [1, 2, 4, 6, 8, 12]
+    prev = 0
+    for kv in range(1, 3001):
+        p = r.parts_bucket(kv)
+        assert p * r.part_tokens >= kv and p in r.parts_buckets and p >= prev
+        prev = p
+    assert r.parts_bucket(1) == 1 and r.parts_bucket(257) == 2 and r.parts_bucket(1025) == 6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("buckets", [None, ()])
+def test_graph_parts_buckets_equal_eager(buckets):
+    """Contexts crossing partition boundaries mid-generation (256 / 512 / 1024 tokens) replay
+    graphs of several partition buckets - token-for-token equal to eager decode."""
+    rng = np.random.default_rng(5)
+    prompts = [rng.integers(300, 30000, size=n).tolist() for n in (250, 505, 1020, 30)]
+    res = []
+    for graphs in (False, True):
+        cfg = EngineConfig(model="small", device="cuda", max_model_len=2048, num_kv_blocks=1024,
+                           max_num_seqs=8, use_graphs=graphs, graph_batch_sizes=(1, 2, 4, 8))
+        if buckets is not None:
+            cfg.graph_parts_buckets = buckets
+        eng = LLMEngine(cfg)
+        # staggered finishes: the longest context leaves first, so the step's bucket walks
+        # 4 -> 6 (1024 crossed) -> 4 -> 2 -> 1
+        sp = [SamplingParams(temperature=0.7, max_tokens=n, ignore_eos=True, seed=7 + i)
+              for i, n in enumerate((24, 14, 8, 30))]
+        outs = eng.generate(prompts, sp)
+        res.append([o.token_ids for o in outs])
+        if graphs and buckets is None:
+            parts = {k[1] for k in eng.runner.graphs}
+            assert len(parts) >= 3, sorted(eng.runner.graphs)
+    assert res[0] == res[1]
+
+
+def _special_params(n):
+    # mixed batch: plain, top-p, top-k, both, greedy
+    mk = [dict(), dict(top_p=0.9), dict(top_k=40), dict(top_p=0.8, top_k=100),
+          dict(temperature=0.0, top_p=0.5)]
+    return [SamplingParams(**{"temperature": 0.7, "max_tokens": 10, "ignore_eos": True,
+                              "seed": 50 + i, **mk[i % len(mk)]}) for i in range(n)]
+
+
+def test_reference_topkp_semantics():
+    """The reference top-k / top-p sampler: filters off == the plain sampler, top_k = 1 and a
+    tiny top_p are argmax, and draws stay inside the nucleus."""
+    from agentic_traffic_testing_amd.ops import reference as ref
+    torch.manual_seed(1)
+    B, V = 64, 50
+    logits = torch.randn(B, V) * 2
+    temp = torch.full((B,), 0.5)
+    seeds = torch.arange(B, dtype=torch.int64)
+    steps = torch.zeros(B, dtype=torch.int64)
+    off = ref.sample_topkp(logits, temp, torch.ones(B), torch.zeros(B, dtype=torch.int32),
+                           seeds, steps)
+    assert torch.equal(off, ref.sample(logits, temp, seeds, steps))
+    k1 = ref.sample_topkp(logits, temp, torch.ones(B), torch.ones(B, dtype=torch.int32),
+                          seeds, steps)
+    assert torch.equal(k1, logits.argmax(-1))
+    p0 = ref.sample_topkp(logits, temp, torch.full((B,), 1e-6), torch.zeros(B, dtype=torch.int32),
+                          seeds, steps)
+    assert torch.equal(p0, logits.argmax(-1))
+    toks = ref.sample_topkp(logits, temp, torch.full((B,), 0.6), torch.zeros(B, dtype=torch.int32),
+                            seeds, steps)
+    for r in range(B):
+        pr = torch.softmax(logits[r] / 0.5, -1)
+        order = torch.argsort(pr, descending=True)
+        n = int((torch.cumsum(pr[order], 0) < 0.6).sum()) + 1
+        assert int(toks[r]) in order[:n + 1].tolist()  # (+1: fixed-point boundary slack)
+
+
+def test_special_sampling_cpu_deterministic():
+    """top-p / top-k requests go through the top-k / top-p sampler (no per-row Python loop):
+    seeded requests replay identically, and top_k = 1 is greedy."""
+    cfg = EngineConfig(model="tiny", device="cpu", max_model_len=256, num_kv_blocks=64,
+                       max_num_seqs=8, use_graphs=False)
+    prompts = _prompts()
+    res = []
+    for _ in range(2):
+        eng = LLMEngine(cfg)
+        outs = eng.generate(prompts, _special_params(len(prompts)))
+        res.append([o.token_ids for o in outs])
+    assert res[0] == res[1]
+    eng = LLMEngine(cfg)
+    sp1 = SamplingParams(temperature=0.9, top_k=1, max_tokens=6, ignore_eos=True, seed=3)
+    sp0 = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
+    a = eng.generate(prompts[:2], sp1)
+    b = eng.generate(prompts[:2], sp0)
+    assert [o.token_ids for o in a] == [o.token_ids for o in b]
+
+
+@pytest.mark.gpu
+def test_special_sampling_graphs_equal_eager():
+    """Mixed plain / top-p / top-k batches replay from hipGraphs (special variant) and equal
+    the eager steps token-for-token."""
+    res = []
+    for graphs in (False, True):
+        cfg = EngineConfig(model="small", device="cuda", max_model_len=512, num_kv_blocks=512,
+                           max_num_seqs=8, use_graphs=graphs, graph_batch_sizes=(1, 2, 4, 8))
+        eng = LLMEngine(cfg)
+        outs = eng.generate(_prompts(vocab=30000), _special_params(5))
+        res.append([o.token_ids for o in outs])
+        if graphs:
+            assert any(k[2] == 1 for k in eng.runner.graphs), sorted(eng.runner.graphs)
+            assert eng.runner.graph_steps > 0
+    assert res[0] == res[1]
+
+
 @pytest.mark.gpu
 def test_fp8_engine_gpu():
     """fp8 weights end to end: graph decode == eager decode, and the fp8 model's greedy

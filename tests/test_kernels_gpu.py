@@ -245,6 +245,72 @@ def test_sample_distribution():
     assert float((freq - p).abs().max()) < 0.03
 
 
+def test_sample_topkp_matches_reference():
+    """Native top-k / top-p sampler vs the reference definition (exact radix-select
+    thresholds, same Gumbel draw); rows with both filters off == the plain sampler."""
+    torch.manual_seed(8)
+    B, V = 12, 128256
+    logits = torch.randn(B, V, device="cuda") * 3
+    logits[5, 100:110] = 9.0  # a tie group straddling the top-k / top-p boundary
+    temp = torch.tensor([0.5, 0.2, 1.0, 0.0, 0.7, 1.0, 0.5, 2.0, 0.5, 1.0, 0.25, 1.0],
+                        device="cuda")
+    top_p = torch.tensor([1.0, 0.9, 0.5, 0.9, 1.0, 0.95, 0.1, 0.99, 1.0, 0.0, 0.8, 1.0],
+                         device="cuda")
+    top_k = torch.tensor([0, 0, 0, 5, 50, 4, -1, 1000, 1, 20, 128255, 128256],
+                         dtype=torch.int32, device="cuda")
+    seeds = torch.arange(B, dtype=torch.int64, device="cuda") * 131 + 7
+    steps = torch.arange(B, dtype=torch.int64, device="cuda") * 5
+    got = ops.sample_topkp(logits, temp, top_p, top_k, seeds, steps).cpu()
+    exp = ref.sample_topkp(logits.cpu(), temp.cpu(), top_p.cpu(), top_k.cpu(), seeds.cpu(),
+                           steps.cpu())
+    # fast-math Gumbel logs may flip a near-tie; the bulk must agree
+    assert int((got == exp).sum()) >= B - 1, (got, exp)
+    # top-k = 1 and top-p = 0 are argmax whatever the noise
+    assert int(got[8]) == int(torch.argmax(logits[8])) and int(got[9]) == int(torch.argmax(logits[9]))
+    # both filters off: bit-identical to the plain sampler (same noise, same tie-break)
+    plain = ops.sample(logits, temp, seeds, steps).cpu()
+    for r in (0, 11):
+        assert int(got[r]) == int(plain[r])
+    # bf16 logits, deterministic
+    l16 = logits.to(torch.bfloat16)
+    a = ops.sample_topkp(l16, temp, top_p, top_k, seeds, steps).cpu()
+    b = ops.sample_topkp(l16, temp, top_p, top_k, seeds, steps).cpu()
+    assert torch.equal(a, b)
+
+
+def test_sample_topkp_distribution():
+    """Draws stay inside the kept set and follow the renormalised softmax over it."""
+    V, N = 16, 6000
+    logits = torch.linspace(-2, 2, V, device="cuda").repeat(N, 1)
+    temp = torch.full((N,), 0.8, device="cuda")
+    seeds = torch.full((N,), 42, dtype=torch.int64, device="cuda")
+    steps = torch.arange(N, dtype=torch.int64, device="cuda")
+    p = torch.softmax(logits[0].cpu() / 0.8, -1)
+    # top-k 4: the 4 largest
+    toks = ops.sample_topkp(logits, temp, torch.ones(N, device="cuda"),
+                            torch.full((N,), 4, dtype=torch.int32, device="cuda"), seeds,
+                            steps).cpu()
+    freq = torch.bincount(toks, minlength=V).float() / N
+    assert float(freq[:12].sum()) == 0.0
+    q = p.clone()
+    q[:12] = 0
+    q /= q.sum()
+    assert float((freq - q).abs().max()) < 0.03
+    # top-p 0.7: smallest top set with mass >= 0.7
+    toks = ops.sample_topkp(logits, temp, torch.full((N,), 0.7, device="cuda"),
+                            torch.zeros(N, dtype=torch.int32, device="cuda"), seeds, steps).cpu()
+    order = torch.argsort(p, descending=True)
+    n_keep = int((torch.cumsum(p[order], 0) < 0.7).sum()) + 1
+    keep = order[:n_keep]
+    freq = torch.bincount(toks, minlength=V).float() / N
+    mask = torch.zeros(V, dtype=torch.bool)
+    mask[keep] = True
+    assert float(freq[~mask].sum()) == 0.0
+    q = torch.where(mask, p, torch.zeros(()))
+    q /= q.sum()
+    assert float((freq - q).abs().max()) < 0.03
+
+
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("m,n,k", [(1, 6144, 4096), (5, 4096, 4096), (12, 28672, 4096),
                                    (16, 4096, 14336), (3, 128256, 4096), (24, 1024, 3584),
@@ -432,6 +498,29 @@ def test_attention_decode_v2(hq, hkv, part_tokens):
                                 part_tokens, out=out)
         close(out[:-1], exp[:-1], 1.5e-2, 2e-2)
         assert bool((cnt == 0).all())
+
+
+def test_attention_decode_v2_grid_invariant():
+    """The partition grid (decode graphs are captured per partition bucket) must not change a
+    single bit: a grid of exactly the partitions needed, one more, and max_model_len's."""
+    torch.manual_seed(12)
+    dt, bs, hq, hkv = torch.bfloat16, 16, 32, 8
+    seqs = [(510, 1), (1025, 1), (264, 1), (54, 1)]
+    k, v, bt, kvlen, qstart, T = _make_paged([(kv, q) for kv, q in seqs], hkv, bs, dt)
+    q = torch.randn(T, hq, 128, dtype=dt, device="cuda")
+    S, scale = len(seqs), 1 / math.sqrt(128)
+    outs = []
+    for max_parts in (5, 6, 8, 32):
+        po = torch.full((S * hkv * max_parts * 16 * 128,), float("nan"), device="cuda")
+        pl = torch.full((S * hkv * max_parts * 16,), float("nan"), device="cuda")
+        cnt = torch.zeros(S * hkv, dtype=torch.int32, device="cuda")
+        out = torch.full_like(q, 3.0)
+        ops.attention_decode_v2(q, k, v, bt, kvlen, qstart, scale, po, pl, cnt, max_parts, 256,
+                                out=out)
+        torch.cuda.synchronize()
+        outs.append(out)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
 
 
 @pytest.mark.parametrize("m", [1, 5, 20])
