@@ -107,9 +107,29 @@ def start_background(handler_cls, host: str = "127.0.0.1", port: int = 0):
 
 
 # ---- clients ---------------------------------------------------------------------------
+_SSL_CTX = None
+_SSL_LOCK = threading.Lock()
+
+
+def shared_ssl_context():
+    """One TLS context for every per-call client.  ``httpx.post`` builds a client per call,
+    and a client built without one loads the CA bundle again: ~65 ms of GIL-holding CPU per
+    call, 13 calls per agentic_parallel task - about 0.8 s of a ~5 s task on the serving
+    host (bench --via http).  The per-call TCP connection is unchanged."""
+    global _SSL_CTX
+    if _SSL_CTX is None:
+        with _SSL_LOCK:
+            if _SSL_CTX is None:
+                import ssl
+
+                _SSL_CTX = ssl.create_default_context()
+    return _SSL_CTX
+
+
 def post_json_new_conn(url: str, payload: dict, headers: dict | None, timeout: float) -> dict:
     """One request on a fresh TCP connection (the reference's module-level httpx.post)."""
-    r = httpx.post(url, json=payload, headers=headers, timeout=timeout)
+    r = httpx.post(url, json=payload, headers=headers, timeout=timeout,
+                   verify=shared_ssl_context())
     r.raise_for_status()
     return r.json()
 

@@ -26,6 +26,7 @@ from .fanout import TASKS
 
 def run_e2e(engine, steps: int, warmup: int, fanout: int = 5, max_tokens: int = 512,
             log=None) -> dict:
+    from ..agents.common.http import shared_ssl_context
     from ..testing.stack import Stack
 
     env = {"LLM_MAX_TOKENS": str(max_tokens), "LLM_IGNORE_EOS": "1", "LLM_TEMPERATURE": "0.2",
@@ -42,7 +43,8 @@ def run_e2e(engine, steps: int, warmup: int, fanout: int = 5, max_tokens: int = 
                 t0 = time.perf_counter()
                 r = httpx.post(url, json={"task": TASKS[i % len(TASKS)] + f" (run {i})",
                                           "scenario": "agentic_parallel",
-                                          "agent_count": fanout}, timeout=1200)
+                                          "agent_count": fanout}, timeout=1200,
+                               verify=shared_ssl_context())
                 r.raise_for_status()
                 body = r.json()
                 metas = [q.get("llm_meta") or {} for q in body.get("llm_requests", [])]
