@@ -95,6 +95,13 @@ MODEL_PRESETS: dict[str, ModelConfig] = {
                             eos_token_ids=(3841, 3849)),
     # 70B attention geometry (GQA 8:1, hidden 8192) with few layers / a small FFN and vocab:
     # the G=8 decode path and 8192-wide GEMVs on one GPU in seconds
+    # Llama-3.2-3B geometry (reference infra/.env.example:116): hidden 3072, 24 q / 8 kv heads
+    # (GQA G = 3), tied embeddings - 2 layers and a small vocab for GPU tests
+    "llama-3b-slice": ModelConfig(name="llama-3b-slice", vocab_size=16384, hidden_size=3072,
+                                  intermediate_size=8192, num_layers=2, num_heads=24,
+                                  num_kv_heads=8, tie_word_embeddings=True,
+                                  rope_scaling=dict(LLAMA3_ROPE_SCALING, factor=32.0),
+                                  bos_token_id=16000, eos_token_ids=(16001, 16009)),
     "llama-70b-slice": ModelConfig(name="llama-70b-slice", vocab_size=16384, hidden_size=8192,
                                    intermediate_size=3584, num_layers=2, num_heads=64,
                                    num_kv_heads=8, rope_scaling=None,

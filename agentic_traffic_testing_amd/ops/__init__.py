@@ -164,9 +164,11 @@ PREFILL_IMPL = os.environ.get("ATTA_PREFILL_IMPL", "flash")
 
 def prefill_tile_tokens(g: int, impl: str | None = None) -> int:
     """Query tokens per prefill attention workgroup for GQA group ``g``."""
+    # 4 waves x (32 // g) tokens (flash: 32 columns per wave) or x (16 // g) (v1: 16) - the
+    # G heads of a token share a wave; G = 3 (Llama-3.2-3B) leaves 2 resp. 1 columns idle
     if (impl or PREFILL_IMPL) == "flash":
-        return 128 // g
-    return PREFILL_TILE_TOKENS.get(g, 16)
+        return 4 * (32 // g)
+    return 4 * (16 // g)
 
 
 def attention_prefill(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, tile_seq,
@@ -227,7 +229,6 @@ def sample(logits, temperature, seeds, steps, out=None):
     return out
 
 
-PREFILL_TILE_TOKENS = {1: 64, 2: 32, 4: 16, 8: 8}  # tokens per prefill workgroup by GQA group
 
 # skinny-GEMM (decode) dispatch: rows <= SKINNY_MAX_M use the MFMA weight-streaming kernel,
 # larger M (prefill) goes to hipBLASLt through F.linear.
@@ -506,7 +507,7 @@ def fused_qkv_attention_ok(x, w, n_q_heads, n_kv_heads, k_cache, max_parts, pres
     g = n_q_heads // n_kv_heads
     step = 256 if w_scale is not None else 128
     return (x.is_cuda and (preshuffled or w_scale is not None) and 1 <= x.shape[0] <= 32
-            and x.shape[1] % step == 0 and n_q_heads % n_kv_heads == 0 and g in (1, 2, 4, 8)
+            and x.shape[1] % step == 0 and n_q_heads % n_kv_heads == 0 and g in (1, 2, 3, 4, 8)
             and 1 <= max_parts <= 64 and k_cache.shape[2] >= 16)
 
 
@@ -574,6 +575,13 @@ def decode_lm_head_sample(x, w, eps, temperature, seeds, steps, keys, tokens=Non
 def key_to_token(keys: torch.Tensor) -> torch.Tensor:
     """Decode signed-orderable packed sampler keys (``finalize="key"``) to token ids."""
     return 0xFFFFFFFF - (keys & 0xFFFFFFFF)
+
+
+def set_attention_trace(trace=None):
+    """Per-workgroup timeline of the decode attention launches that follow (int64 CUDA tensor
+    of 4 words per workgroup of the (seqs, kv heads, partitions) grid: past round trip 1,
+    computed, published, end - 100 MHz wall clock); None switches it off."""
+    _native().set_attention_trace(trace)
 
 
 def attention_decode_v2(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, scale,

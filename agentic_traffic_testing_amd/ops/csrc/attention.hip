@@ -317,6 +317,7 @@ static void launch_attn(const AttnParams& prm, int G, dim3 grid, hipStream_t str
   switch (G) {
     case 1: paged_attention_kernel<T, 1, kSplit><<<grid, 256, 0, stream>>>(prm); break;
     case 2: paged_attention_kernel<T, 2, kSplit><<<grid, 256, 0, stream>>>(prm); break;
+    case 3: paged_attention_kernel<T, 3, kSplit><<<grid, 256, 0, stream>>>(prm); break;
     case 4: paged_attention_kernel<T, 4, kSplit><<<grid, 256, 0, stream>>>(prm); break;
     case 8: paged_attention_kernel<T, 8, kSplit><<<grid, 256, 0, stream>>>(prm); break;
     default: break;
@@ -341,7 +342,7 @@ int atta_attention_prefill(void* out, const void* q, const void* k_cache, const 
                            int dtype, hipStream_t stream) {
   const int G = n_q_heads / n_kv_heads;
   const int shift = bs_to_shift(block_size);
-  if (head_dim != kD || shift < 0 || n_q_heads % n_kv_heads != 0 || (G & (G - 1)) || G > 8)
+  if (head_dim != kD || shift < 0 || n_q_heads % n_kv_heads != 0 || ((G & (G - 1)) && G != 3) || G > 8)
     return -1;
   if (num_tiles == 0) return 0;
   AttnParams prm{};
@@ -378,7 +379,7 @@ int atta_attention_decode(void* out, float* part_out, float* part_lse, const voi
                           int64_t out_stride, float scale, int dtype, hipStream_t stream) {
   const int G = n_q_heads / n_kv_heads;
   const int shift = bs_to_shift(block_size);
-  if (head_dim != kD || shift < 0 || n_q_heads % n_kv_heads != 0 || (G & (G - 1)) || G > 8)
+  if (head_dim != kD || shift < 0 || n_q_heads % n_kv_heads != 0 || ((G & (G - 1)) && G != 3) || G > 8)
     return -1;
   if (part_tokens % 64 != 0 || num_parts < 1) return -1;
   if (num_seqs == 0) return 0;

@@ -122,8 +122,7 @@ __device__ __forceinline__ void fused_exit(const DecParams& p, int hk) {
 template <typename T, int G, int WAVES, int TPW, bool FUSED>
 __device__ __forceinline__ void decode_attention_body(const DecParams& p, const int s,
                                                       const int hk, const int part,
-                                                      unsigned long long& t_start,
-                                                      unsigned long long& t_wait) {
+                                                      unsigned long long (&tr)[3]) {
   using frag8 = typename Mf<T>::frag8;
   __shared__ float lds_o[WAVES][G][kD + 4];
   __shared__ float lds_m[WAVES][G];
@@ -156,7 +155,7 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
   for (int i = 0; i < TPW; ++i) asm volatile("" : "+s"(bte[i]));
   // timeline probe (fused launch): clock reads only after the scalar loads above - an
   // earlier one makes them vector loads, which the scalar-operand asm cannot take
-  if constexpr (FUSED) t_start = wall_clock64();
+  tr[0] = wall_clock64();
   const int nparts = (kvlen + PT - 1) / PT;
   if (part >= nparts) {  // block-uniform (also kvlen == 0 dummy sequences)
     if constexpr (FUSED) fused_exit(p, hk);
@@ -204,7 +203,7 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
     // the cache tiles above are in flight; now wait for this KV head's q / k / v producers
     if (threadIdx.x == 0) wait_count(p.pub_counters + hk, p.pub_target, p.error_word, p.poll_sleeps);
     __syncthreads();
-    t_wait = wall_clock64();  // timeline probe (stored at exit)
+    tr[1] = wall_clock64();  // timeline probe (stored at exit)
     // device-scope loads of the handed-off rows (written 16 B write-through by producers)
     const bool ok = col < G;
     const auto rq = dev_rsrc(p.q);
@@ -288,6 +287,7 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
     }
   }
   if constexpr (FUSED) fused_exit(p, hk);  // past its wait: the hand-off words may re-arm
+  else tr[1] = wall_clock64();
 
   // ---- merge the WAVES partial states (only the G valid columns) ---------------------------
   if (col < G) {
@@ -358,45 +358,80 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
     lds_last = (old == nparts - 1);
   }
   __syncthreads();
+  tr[2] = wall_clock64();
   if (!lds_last) return;
-  // merge: every merger thread streams (lse, partial) of 4 partitions per round trip and
-  // folds them into a running (max, weight sum, weighted sum) - one round trip for <= 4
-  // partitions (1k tokens at 256-token partitions)
-  if (merger) {
+  // merge in one round trip for <= 4 * NG partitions: the workgroup's threads form NG merge
+  // groups of G * 16 (one thread per (head, 8 dims)); group g loads partitions g, g + NG, ...
+  // (4 per round trip) and folds them into a running (max, weight sum, weighted sum); the
+  // group states meet in LDS and group 0 folds them in group order (fixed order: the
+  // output does not depend on timing or on the launch's partition grid).  Was: the 64
+  // merger threads alone, 4 partitions per dependent round trip (12 partitions at 3k tokens
+  // = 3 round trips).
+  {
+    constexpr int MG = G * 16;
+    constexpr int NG_ALL = WAVES * 64 / MG;
+    constexpr int NG = NG_ALL < 16 ? NG_ALL : 16;
+    __shared__ float lds_mg[NG][10][MG];
+    const int gidx = threadIdx.x / MG;
+    const int lt = threadIdx.x % MG;
+    const int mc = lt >> 4;
+    const int md0 = (lt & 15) * 8;
     const int np = min(nparts, 64);
     float m_run = kNegInf, wsum = 0.f;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int q0 = 0; q0 < np; q0 += 4) {
-      float lse[4];
-      f32x4 pa[4], pb[4];
+    if (gidx < NG) {
+      for (int u0 = 0; gidx + NG * u0 < np; u0 += 4) {
+        float lse[4];
+        f32x4 pa[4], pb[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t base = (sh * p.max_parts + min(q0 + u, np - 1)) * 16 + c;
-        const uint32_t off = static_cast<uint32_t>((base * kD + d0) * 4);
-        lse[u] = dev_load4(rpl, static_cast<uint32_t>(base * 4));
-        pa[u] = __builtin_bit_cast(f32x4, dev_load16(rpo, off));
-        pb[u] = __builtin_bit_cast(f32x4, dev_load16(rpo, off + 16));
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (q0 + u >= np || lse[u] == kNegInf) continue;  // lse == -inf -> weight 0
-        const float m_new = fmaxf(m_run, lse[u]);
-        const float sc = exp2f(m_run - m_new);  // m_run == -inf -> 0
-        const float w = exp2f(lse[u] - m_new);
-        wsum = wsum * sc + w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc[j] = acc[j] * sc + w * pa[u][j];
-          acc[4 + j] = acc[4 + j] * sc + w * pb[u][j];
+        for (int u = 0; u < 4; ++u) {
+          const int q = min(gidx + NG * (u0 + u), np - 1);
+          const int64_t base = (sh * p.max_parts + q) * 16 + mc;
+          const uint32_t off = static_cast<uint32_t>((base * kD + md0) * 4);
+          lse[u] = dev_load4(rpl, static_cast<uint32_t>(base * 4));
+          pa[u] = __builtin_bit_cast(f32x4, dev_load16(rpo, off));
+          pb[u] = __builtin_bit_cast(f32x4, dev_load16(rpo, off + 16));
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (gidx + NG * (u0 + u) >= np || lse[u] == kNegInf) continue;  // weight 0
+          const float m_new = fmaxf(m_run, lse[u]);
+          const float sc = exp2f(m_run - m_new);  // m_run == -inf -> 0
+          const float w = exp2f(lse[u] - m_new);
+          wsum = wsum * sc + w;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            acc[jj] = acc[jj] * sc + w * pa[u][jj];
+            acc[4 + jj] = acc[4 + jj] * sc + w * pb[u][jj];
+          }
+          m_run = m_new;
+        }
+      }
+      lds_mg[gidx][0][lt] = m_run;
+      lds_mg[gidx][1][lt] = wsum;
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) lds_mg[gidx][2 + jj][lt] = acc[jj];
+    }
+    __syncthreads();
+    if (gidx == 0) {
+      for (int g = 1; g < NG; ++g) {
+        const float gm = lds_mg[g][0][lt];
+        if (gm == kNegInf) continue;
+        const float m_new = fmaxf(m_run, gm);
+        const float sc = exp2f(m_run - m_new);
+        const float w = exp2f(gm - m_new);
+        wsum = wsum * sc + w * lds_mg[g][1][lt];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) acc[jj] = acc[jj] * sc + w * lds_mg[g][2 + jj][lt];
         m_run = m_new;
       }
-    }
-    const float inv = wsum > 0.f ? 1.f / wsum : 0.f;
-    Pack8 o8;
+      const float inv = wsum > 0.f ? 1.f / wsum : 0.f;
+      Pack8 o8;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o8.v[j] = from_f32<T>(acc[j] * inv);
-    *reinterpret_cast<Pack8*>(outp) = o8;
+      for (int jj = 0; jj < 8; ++jj) o8.v[jj] = from_f32<T>(acc[jj] * inv);
+      *reinterpret_cast<Pack8*>(p.out + static_cast<int64_t>(qrow) * p.out_stride +
+                                static_cast<int64_t>(hk * G + mc) * kD + md0) = o8;
+    }
   }
   if (threadIdx.x == 0)
     __hip_atomic_store(p.counters + sh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -404,9 +439,17 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
 
 template <typename T, int G, int WAVES, int TPW>
 __global__ __launch_bounds__(WAVES * 64) void decode_attention_kernel(DecParams p) {
-  unsigned long long t_start, t_wait;
-  decode_attention_body<T, G, WAVES, TPW, false>(p, blockIdx.x, blockIdx.y, blockIdx.z, t_start,
-                                                 t_wait);
+  unsigned long long tr[3] = {0, 0, 0};
+  decode_attention_body<T, G, WAVES, TPW, false>(p, blockIdx.x, blockIdx.y, blockIdx.z, tr);
+  // timeline probe (set_attention_trace): [past round trip 1, computed, published, end]
+  if (p.wg_trace != nullptr && threadIdx.x == 0) {
+    const int64_t b = blockIdx.x + static_cast<int64_t>(gridDim.x) *
+                                       (blockIdx.y + static_cast<int64_t>(gridDim.y) * blockIdx.z);
+    p.wg_trace[4 * b] = tr[0];
+    p.wg_trace[4 * b + 1] = tr[1];
+    p.wg_trace[4 * b + 2] = tr[2];
+    p.wg_trace[4 * b + 3] = wall_clock64();
+  }
 }
 
 template <typename T, int WAVES, int TPW>
@@ -414,6 +457,7 @@ static int launch_g(int G, dim3 grid, hipStream_t st, const DecParams& p) {
   switch (G) {
     case 1: decode_attention_kernel<T, 1, WAVES, TPW><<<grid, WAVES * 64, 0, st>>>(p); return 0;
     case 2: decode_attention_kernel<T, 2, WAVES, TPW><<<grid, WAVES * 64, 0, st>>>(p); return 0;
+    case 3: decode_attention_kernel<T, 3, WAVES, TPW><<<grid, WAVES * 64, 0, st>>>(p); return 0;
     case 4: decode_attention_kernel<T, 4, WAVES, TPW><<<grid, WAVES * 64, 0, st>>>(p); return 0;
     case 8: decode_attention_kernel<T, 8, WAVES, TPW><<<grid, WAVES * 64, 0, st>>>(p); return 0;
     default: return -1;
@@ -450,6 +494,7 @@ __global__ __launch_bounds__(256) void qkv_attn_kernel(SkinnyParams sp, DecParam
   // timeline probe: every store at the exit - a store ahead of the bodies' loads would let
   // them alias it and demote their scalar loads to vector ones
   unsigned long long t0 = 0, t_wait = 0;
+  unsigned long long tr[3] = {0, 0, 0};
   if (b < n_tiles) {
     t0 = wall_clock64();
     skinny_body<T, 4, W8 ? 8 : 4, MT, EPI_QKVPUB, true, true, W8>(sp, b, 0);
@@ -458,7 +503,9 @@ __global__ __launch_bounds__(256) void qkv_attn_kernel(SkinnyParams sp, DecParam
     const int part = a % att_parts;
     const int hk = (a / att_parts) % dp.n_kv_heads;
     const int s = a / (att_parts * dp.n_kv_heads);
-    decode_attention_body<T, G, 4, 4, true>(dp, s, hk, part, t0, t_wait);
+    decode_attention_body<T, G, 4, 4, true>(dp, s, hk, part, tr);
+    t0 = tr[0];
+    t_wait = tr[1];
   }
   if (dp.wg_trace != nullptr && threadIdx.x == 0) {
     dp.wg_trace[4 * b] = t0;
@@ -474,6 +521,7 @@ static int launch_fused_g(int G, dim3 grid, hipStream_t st, const SkinnyParams& 
   switch (G) {
     case 1: qkv_attn_kernel<T, 1, MT, W8><<<grid, 256, 0, st>>>(sp, dp, n_tiles, parts); return 0;
     case 2: qkv_attn_kernel<T, 2, MT, W8><<<grid, 256, 0, st>>>(sp, dp, n_tiles, parts); return 0;
+    case 3: qkv_attn_kernel<T, 3, MT, W8><<<grid, 256, 0, st>>>(sp, dp, n_tiles, parts); return 0;
     case 4: qkv_attn_kernel<T, 4, MT, W8><<<grid, 256, 0, st>>>(sp, dp, n_tiles, parts); return 0;
     case 8: qkv_attn_kernel<T, 8, MT, W8><<<grid, 256, 0, st>>>(sp, dp, n_tiles, parts); return 0;
     default: return -1;
@@ -494,6 +542,13 @@ static int launch_fused(int G, int mt, bool w8, dim3 grid, hipStream_t st, const
 
 using namespace atta;
 
+static unsigned long long* g_attn_trace = nullptr;
+
+// Timeline probe for the decode attention launches that follow (nullptr: off).
+void atta_set_attention_trace(void* trace) {
+  g_attn_trace = static_cast<unsigned long long*>(trace);
+}
+
 int atta_attention_decode_v2(void* out, float* part_out, float* part_lse, int* counters,
                              const void* q, const void* k_cache, const void* v_cache,
                              const int* block_tables, const int* seq_kvlen, const int* seq_qstart,
@@ -505,7 +560,7 @@ int atta_attention_decode_v2(void* out, float* part_out, float* part_lse, int* c
   int shift = 0;
   while ((1 << shift) < block_size) ++shift;
   if (head_dim != 128 || (1 << shift) != block_size || block_size < 16) return -1;
-  if (n_q_heads % n_kv_heads || G > 8 || (G & (G - 1))) return -1;
+  if (n_q_heads % n_kv_heads || G > 8 || ((G & (G - 1)) && G != 3)) return -1;
   if (max_parts < 1 || max_parts > 64) return -1;
   if (num_seqs == 0) return 0;
   dec::DecParams p{};
@@ -527,6 +582,7 @@ int atta_attention_decode_v2(void* out, float* part_out, float* part_lse, int* c
   p.part_tokens = part_tokens;
   p.max_parts = max_parts;
   p.scale_log2 = scale * 1.4426950408889634f;
+  p.wg_trace = g_attn_trace;
   dim3 grid(num_seqs, n_kv_heads, max_parts);
   const int rc = dtype == 0 ? dec::launch<__bf16>(G, part_tokens, grid, stream, p)
                             : dec::launch<_Float16>(G, part_tokens, grid, stream, p);
@@ -546,7 +602,7 @@ int atta_fused_qkv_attn(void* q_out, void* k_cache, void* v_cache, const void* x
   int shift = 0;
   while ((1 << shift) < block_size) ++shift;
   if ((1 << shift) != block_size || block_size < 16) return -1;
-  if (n_q_heads % n_kv_heads || G > 8 || (G & (G - 1))) return -1;
+  if (n_q_heads % n_kv_heads || G > 8 || ((G & (G - 1)) && G != 3)) return -1;
   if (M < 1 || M > 32 || max_parts < 1 || max_parts > 64) return -1;
   const bool w8 = wscale != nullptr;
   if (K % ((w8 ? 64 : 32) * 4) != 0) return -1;  // 4 waves, whole MFMA K-steps
@@ -605,7 +661,10 @@ int atta_fused_qkv_attn(void* q_out, void* k_cache, void* v_cache, const void* x
   }();
   dp.poll_sleeps = poll_sleeps;
   const int n_tiles = sp.N / 16;
-  dim3 grid(n_tiles + M * n_kv_heads * max_parts);
+  // timing probe only (scripts/gpu/trace_fused_qkv_attn.py): the producer tiles alone - the
+  // hand-off counters are left armed, so results of later launches are garbage
+  static const bool producers_only = getenv("ATTA_FUSED_PRODUCERS_ONLY") != nullptr;
+  dim3 grid(n_tiles + (producers_only ? 0 : M * n_kv_heads * max_parts));
   const int mt = M <= 16 ? 1 : 2;
   const int rc = dtype == 0
                      ? dec::launch_fused<__bf16>(G, mt, w8, grid, stream, sp, dp, n_tiles, max_parts)

@@ -462,6 +462,16 @@ void attention_decode_v2(at::Tensor out, at::Tensor part_out, at::Tensor part_ls
            "attention_decode_v2");
 }
 
+void set_attention_trace(const c10::optional<at::Tensor>& trace) {
+  if (trace.has_value()) {
+    TORCH_CHECK(trace->scalar_type() == at::kLong && trace->is_contiguous() && trace->is_cuda(),
+                "set_attention_trace: int64 cuda tensor");
+    atta_set_attention_trace(trace->data_ptr());
+  } else {
+    atta_set_attention_trace(nullptr);
+  }
+}
+
 void fused_qkv_attn(at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache, const at::Tensor& x,
                     const at::Tensor& w, const at::Tensor& positions, const at::Tensor& slots,
                     const at::Tensor& cos_sin, int64_t n_q_heads, int64_t n_kv_heads, double eps,
@@ -617,6 +627,7 @@ void ar2_run(const at::Tensor& x, at::Tensor y, at::IntArrayRef bases, int64_t r
 TORCH_LIBRARY(atta, m) {
   m.def("ar_buffer_bytes(int max_elems, int elem_bytes) -> int", &ar_buffer_bytes);
   m.def("ar_alloc(int bytes, int device) -> int", &ar_alloc);
+  m.def("set_attention_trace(Tensor? trace) -> ()", &set_attention_trace);
   m.def("ar_free(int ptr) -> ()", &ar_free);
   m.def("ar_handle(int ptr) -> Tensor", &ar_handle);
   m.def("ar_open(Tensor handle) -> int", &ar_open);

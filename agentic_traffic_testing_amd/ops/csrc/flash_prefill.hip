@@ -2,7 +2,8 @@
 // (replaces the attention vLLM runs under engine.generate(), reference
 // llm/serve_llm.py:527-531).  Varlen batches, causal with a context offset (chunked prefill
 // and prefix-cache hits: query token i of a sequence sits at position kvlen - qlen + i),
-// GQA G = Hq / Hkv in {1, 2, 4, 8}, head_dim 128, bf16 / fp16.
+// GQA G = Hq / Hkv in {1, 2, 3, 4, 8}, head_dim 128, bf16 / fp16 (G = 3: Llama-3.2-3B, 24 q /
+// 8 kv heads; a wave's last 32 mod 3 = 2 columns idle).
 //
 // Work decomposition: grid (tiles, Hkv).  A workgroup = 4 waves owns 128 "columns" = the G
 // query heads of one KV head x 128 / G consecutive query tokens of one sequence; wave w owns
@@ -110,7 +111,8 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
   // this lane's column
   const int c_tok = qoff + wid * kTokPerWave + r / G;
   const int c_head = hk * G + r % G;
-  const bool c_valid = c_tok < qlen;
+  // (G = 3: columns 30, 31 of a wave would spill into the next wave's tokens)
+  const bool c_valid = r < kTokPerWave * G && c_tok < qlen;
   const int c_end = c_valid ? ctx0 + c_tok + 1 : 0;  // keys [0, c_end) are visible
   // workgroup key range: up to the last valid token's causal limit
   const int wg_last_tok = min(qoff + kTokPerWg, qlen) - 1;
@@ -309,6 +311,7 @@ static int launch(int G, dim3 grid, hipStream_t st, const FlashParams& p) {
   switch (G) {
     case 1: flash_prefill_kernel<T, 1><<<grid, 256, 0, st>>>(p); return 0;
     case 2: flash_prefill_kernel<T, 2><<<grid, 256, 0, st>>>(p); return 0;
+    case 3: flash_prefill_kernel<T, 3><<<grid, 256, 0, st>>>(p); return 0;
     case 4: flash_prefill_kernel<T, 4><<<grid, 256, 0, st>>>(p); return 0;
     case 8: flash_prefill_kernel<T, 8><<<grid, 256, 0, st>>>(p); return 0;
     default: return -1;
@@ -330,7 +333,7 @@ int atta_flash_prefill(void* out, const void* q, const void* k_cache, const void
   int shift = 0;
   while ((1 << shift) < block_size) ++shift;
   if (head_dim != fp::kD || (1 << shift) != block_size || block_size < 16) return -1;
-  if (n_q_heads % n_kv_heads || G > 8 || (G & (G - 1))) return -1;
+  if (n_q_heads % n_kv_heads || G > 8 || ((G & (G - 1)) && G != 3)) return -1;
   // 16-byte row loads of q / stores of out need 8-element aligned row strides
   if (q_stride % 8 || out_stride % 4) return -1;
   if (num_tiles == 0) return 0;

@@ -83,6 +83,9 @@ int atta_fused_lm_head_sample(int64_t* tokens, unsigned long long* keys, const v
 int atta_sample_finalize(int64_t* tokens, const unsigned long long* keys, int M, int n_tiles,
                          hipStream_t stream);
 
+// per-workgroup timeline of later decode attention launches (int64 [4 x grid]; nullptr off)
+void atta_set_attention_trace(void* trace);
+
 int atta_attention_decode_v2(void* out, float* part_out, float* part_lse, int* counters,
                              const void* q, const void* k_cache, const void* v_cache,
                              const int* block_tables, const int* seq_kvlen, const int* seq_qstart,

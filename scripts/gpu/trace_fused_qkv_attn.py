@@ -103,6 +103,23 @@ def run(ctxs, dt=torch.bfloat16):
     print(f"  separate qkv+attn {timeit(sep):7.2f} us   (qkv {timeit(qkv_only):6.2f}, "
           f"attn {timeit(attn_only):6.2f})")
     print(f"  fused             {timeit(fused):7.2f} us", flush=True)
+    # standalone attention timeline
+    qkv_only()
+    atr = torch.zeros(4 * B * HKV * MAXP, dtype=torch.int64, device="cuda")
+    ops.set_attention_trace(atr)
+    for _ in range(3):
+        attn_only()
+    torch.cuda.synchronize()
+    ops.set_attention_trace(None)
+    t = atr.view(MAXP, HKV, B, 4).cpu()  # grid (seqs, heads, parts): x fastest
+    real = [(s_, h, p_) for s_ in range(B) for h in range(HKV)
+            for p_ in range(math.ceil(kvlens[s_] / 256))]
+    if real:
+        t0a = min(int(t[p_, h, s_, 0]) for s_, h, p_ in real)
+        col = lambda j: sorted((int(t[p_, h, s_, j]) - t0a) / 100.0 for s_, h, p_ in real)  # noqa
+        for j, name in enumerate(("past RT1", "computed", "published", "end")):
+            c = col(j)
+            print(f"  attn {name:9s} p0/p50/max {c[0]:6.2f} {c[len(c) // 2]:6.2f} {c[-1]:6.2f}")
     kv_real = kvlen.clone()
     kvlen.zero_()  # no attention work: the qkv tiles alone inside the fused launch
     print(f"  fused, kvlen 0    {timeit(fused):7.2f} us", flush=True)
@@ -139,8 +156,50 @@ def run(ctxs, dt=torch.bfloat16):
     print(f"  distinct CU ids among qkv tiles: {cus}", flush=True)
 
 
+def producers_only():
+    """ATTA_FUSED_PRODUCERS_ONLY=1: the fused launch with its qkv tiles only (timing)."""
+    B, dt, ncopy = 1, torch.bfloat16, 8
+    x = torch.randn(B, H, dtype=dt, device="cuda")
+    ws_ = [ops.preshuffle(torch.randn((HQ + 2 * HKV) * 128, H, dtype=dt, device="cuda") * 0.02,
+                          "qkv") for _ in range(ncopy)]
+    cs = ref.rope_cos_sin(128, 8192, 500000.0, None, device="cuda")
+    k = torch.zeros(64, HKV, BS, 128, dtype=dt, device="cuda")
+    v = torch.zeros(64, HKV, 128, BS, dtype=dt, device="cuda")
+    bt = torch.zeros(B, 16, dtype=torch.int32, device="cuda")
+    kvlen = torch.zeros(B, dtype=torch.int32, device="cuda")
+    pos = torch.zeros(B, dtype=torch.int32, device="cuda")
+    slots = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+    ws = {"part_out": torch.empty(B * HKV * MAXP * 16 * 128, device="cuda"),
+          "part_lse": torch.empty(B * HKV * MAXP * 16, device="cuda"),
+          "counters": torch.zeros(B * HKV, dtype=torch.int32, device="cuda"),
+          "side_kv": torch.zeros(B, HKV, 2, 128, dtype=dt, device="cuda"),
+          "pub_counters": torch.zeros(HKV, dtype=torch.int32, device="cuda"),
+          "exit_counters": torch.zeros(HKV, dtype=torch.int32, device="cuda"),
+          "fused_error": torch.zeros(1, dtype=torch.int32, device="cuda"),
+          "max_parts": MAXP}
+    q = torch.empty(B, HQ, 128, dtype=dt, device="cuda")
+    a = torch.empty(B, HQ, 128, dtype=dt, device="cuda")
+    i = [0]
+
+    def sep():
+        i[0] = (i[0] + 1) % ncopy
+        ops.decode_qkv_rope(x, ws_[i[0]], 1e-5, pos, slots, cs, k, v, HQ, HKV, q_out=q,
+                            preshuffled=True)
+
+    def fused():
+        i[0] = (i[0] + 1) % ncopy
+        ops.decode_qkv_attention(x, ws_[i[0]], 1e-5, pos, slots, cs, k, v, HQ, HKV, bt, kvlen,
+                                 1.0, ws, q, a)
+
+    print(f"producers only: standalone qkv {timeit(sep):6.2f} us, fused-kernel qkv tiles "
+          f"{timeit(fused):6.2f} us", flush=True)
+
+
 if __name__ == "__main__":
     assert ops.native_available()
+    if os.environ.get("ATTA_FUSED_PRODUCERS_ONLY"):
+        producers_only()
+        sys.exit(0)
     print(f"poll sleeps {os.environ.get('ATTA_FUSED_POLL_SLEEPS', '1')}")
     run([3000])
     if len(sys.argv) < 2:

@@ -298,6 +298,26 @@ def test_70b_geometry_fused_decode(quant):
 
 
 @pytest.mark.gpu
+def test_llama32_3b_geometry():
+    """Llama-3.2-3B geometry - the reference's .env model (infra/.env.example:116): hidden
+    3072, 24 q / 8 kv heads (GQA G = 3, not a power of two), tied embeddings - through the
+    flash prefill, the fused graph decode and the top-k / top-p sampler, against the dense
+    oracle."""
+    cfg = EngineConfig(model="llama-3b-slice", device="cuda", max_model_len=512,
+                       num_kv_blocks=512, max_num_batched_tokens=128, max_num_seqs=8,
+                       graph_batch_sizes=(1, 2, 4, 8))
+    eng = LLMEngine(cfg)
+    m = eng.runner.model
+    assert m.g == 3 and m.cfg.hidden_size == 3072 and m.cfg.tie_word_embeddings
+    outs, bad = _check(eng, _prompts(vocab=16000), n=8, tol_logit=0.25)
+    assert bad <= 2
+    assert eng.runner.graph_steps > 0
+    sp = SamplingParams(temperature=0.8, top_p=0.9, top_k=50, max_tokens=6, ignore_eos=True,
+                        seed=9)
+    assert all(len(o.token_ids) == 6 for o in eng.generate(_prompts(vocab=16000), sp))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("max_len", [11000, 20000])
 def test_long_context_decode(max_len):
     """max_model_len 11000 (reference infra/.env.example:129): a ~10.5k-token prompt through

@@ -77,7 +77,7 @@ def _rand_cache(nb, hkv, bs, d, dtype):
 
 
 @pytest.mark.parametrize("dtype", DT)
-@pytest.mark.parametrize("hq,hkv", [(32, 8), (8, 1), (4, 1)])
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (8, 1), (4, 1), (24, 8)])
 def test_rope_cache(dtype, hq, hkv):
     torch.manual_seed(3)
     T, D, bs, nb = 37, 128, 16, 64
@@ -130,7 +130,7 @@ def _tiles(seqs, tile):
 
 @pytest.mark.parametrize("impl", ["flash", "v1"])
 @pytest.mark.parametrize("dtype", DT)
-@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 1), (4, 1), (16, 16)])
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 1), (4, 1), (16, 16), (24, 8)])
 @pytest.mark.parametrize("bs", [16, 32])
 def test_attention_prefill(impl, dtype, hq, hkv, bs):
     torch.manual_seed(4)
@@ -145,7 +145,7 @@ def test_attention_prefill(impl, dtype, hq, hkv, bs):
     close(got, exp, 1.5e-2, 2e-2)
 
 
-@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8)])
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (24, 8)])
 def test_flash_prefill_long_chunked(hq, hkv):
     """2.6k-token prompt (the fan-out synthesis size) plus a chunk after a 3k cached prefix
     and an 11k-context chunk (reference .env max_model_len 11000): the flash kernel's block
@@ -163,7 +163,7 @@ def test_flash_prefill_long_chunked(hq, hkv):
 
 
 @pytest.mark.parametrize("dtype", DT)
-@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 1), (4, 1)])
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 1), (4, 1), (24, 8)])
 @pytest.mark.parametrize("parts", [1, 4, 16])
 def test_attention_decode(dtype, hq, hkv, parts):
     torch.manual_seed(5)
@@ -387,7 +387,7 @@ def _norm_ref(x, eps=1e-5):
 
 
 @pytest.mark.parametrize("m", [1, 5, 16, 24])
-@pytest.mark.parametrize("hq,hkv", [(32, 8), (8, 1)])
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (8, 1), (24, 8)])
 def test_decode_qkv_rope(m, hq, hkv):
     torch.manual_seed(8)
     dt, H, bs, nb = torch.bfloat16, 4096, 16, 64
@@ -476,7 +476,7 @@ def test_decode_lm_head_sample_vocab_parallel(m):
             float(logits[0, int(ops.key_to_token(ref_keys)[0])])) < 0.05
 
 
-@pytest.mark.parametrize("hq,hkv", [(32, 8), (8, 1), (64, 8)])
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (8, 1), (64, 8), (24, 8)])
 @pytest.mark.parametrize("part_tokens", [128, 256, 512])
 def test_attention_decode_v2(hq, hkv, part_tokens):
     torch.manual_seed(11)
@@ -688,7 +688,7 @@ def _fused_ws(B, hkv, max_parts, dt):
 
 
 @pytest.mark.parametrize("fp8", [False, True])
-@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 1)])
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 1), (24, 8)])
 def test_fused_qkv_attention(fp8, hq, hkv):
     """One launch of qkv(+norm+RoPE+KV write) and decode attention == the two-launch path:
     q / K / V writes bit-identical, attention within fp32-reordering tolerance of the fp32
