@@ -143,6 +143,9 @@ def test_tp_engine_matches_tp1_cpu(tp, model):
                             ref_eng.runner.model.inter)
     exp_g = [o.token_ids for o in ref_eng.generate(_prompts(), greedy)]
     exp_s = [o.token_ids for o in ref_eng.generate(_prompts(), sampled)]
+    topp = SamplingParams(temperature=0.7, top_p=0.9, top_k=40, max_tokens=4, ignore_eos=True,
+                          seed=3)
+    exp_p = [o.token_ids for o in ref_eng.generate(_prompts()[:2], topp)]
     del ref_eng
     eng = TPEngine(EngineConfig(tensor_parallel_size=tp, **base))
     try:
@@ -151,13 +154,13 @@ def test_tp_engine_matches_tp1_cpu(tp, model):
         assert m.kv_rep == max(1, tp // n_kv) and m.n_kv_heads == max(1, n_kv // tp)
         got_g = [o.token_ids for o in eng.generate(_prompts(), greedy)]
         got_s = [o.token_ids for o in eng.generate(_prompts(), sampled)]
-        # top-p path: rank 0 samples, the workers only join the logits all-gather
-        topp = SamplingParams(temperature=0.7, top_p=0.9, max_tokens=4, ignore_eos=True, seed=3)
-        assert all(len(o.token_ids) == 4 for o in eng.generate(_prompts()[:2], topp))
+        # top-k / top-p: every rank samples the all-gathered logits with the same kernel
+        got_p = [o.token_ids for o in eng.generate(_prompts()[:2], topp)]
     finally:
         eng.shutdown()
     assert got_g == exp_g
     assert got_s == exp_s
+    assert got_p == exp_p
     assert not any(p.is_alive() for p in eng.procs)
 
 
@@ -242,6 +245,10 @@ def test_tp2_same_gpu_rehearsal(allreduce):
                                 tp_allreduce=allreduce, **base))
     try:
         got = [o.token_ids for o in eng.generate(_prompts(), greedy)]
+        # top-k / top-p on real kernels: every rank samples the all-gathered logits
+        topp = SamplingParams(temperature=0.7, top_p=0.9, top_k=40, max_tokens=4,
+                              ignore_eos=True, seed=5)
+        assert all(len(o.token_ids) == 4 for o in eng.generate(_prompts()[:2], topp))
         if allreduce == "ipc":
             assert eng.comm.ipc is not None and eng.comm.ipc.calls > 0
             assert eng.comm.ipc.check() == 0
