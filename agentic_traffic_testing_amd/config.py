@@ -187,11 +187,6 @@ class EngineConfig:
     long_prefill_token_threshold: int = 0
     # fused native decode path (GEMV kernels) when available
     fused_decode: bool = True
-    # fused decode qkv GEMV + attention in one launch (the attention's cached-context loads
-    # under the qkv weight stream, q / new k,v handed over in-launch).  Off: measured slower
-    # in the decode step (29.3 us vs 11.8 + 8.6 us for the two launches,
-    # profiles/r2_fused_qkv_attn_experiment.txt); kept, tested, for A/B runs
-    fuse_qkv_attn: bool = False
     # async look-ahead decode: launch the next decode graph step before waiting for the
     # current one's tokens (llm_engine.LLMEngine.step)
     async_decode: bool = True

@@ -190,13 +190,6 @@ class ModelRunner:
             "tokens": torch.zeros(self.max_seqs, dtype=torch.int64, device=dev),
             "tp_keys": torch.zeros(self.max_seqs, dtype=torch.int64, device=dev),
             "counters": torch.zeros(self.max_seqs * nkv, dtype=torch.int32, device=dev),
-            # fused qkv + attention hand-off: new-token k / v rows, per-KV-head arrival and
-            # exit counters (zeroed once, re-armed in-kernel), bounded-wait error word
-            "side_kv": torch.zeros(self.max_seqs, nkv, 2, 128, dtype=dt, device=dev),
-            "pub_counters": torch.zeros(nkv, dtype=torch.int32, device=dev),
-            "exit_counters": torch.zeros(nkv, dtype=torch.int32, device=dev),
-            "fused_error": torch.zeros(1, dtype=torch.int32, device=dev),
-            "fuse_qkv_attn": bool(cfg.fuse_qkv_attn) and self.part_tokens == 256,
             "part_out": self.part_out, "part_lse": self.part_lse,
             "max_parts": self.max_parts, "part_tokens": self.part_tokens,
         }
@@ -257,10 +250,6 @@ class ModelRunner:
         self.k_layers = [self.k_cache[i] for i in range(L)]
         self.v_layers = [self.v_cache[i] for i in range(L)]
         self.kv_bytes = per_block * nb
-
-    def fused_error(self) -> int:
-        """Nonzero when a fused qkv+attention wait timed out (results were garbage)."""
-        return int(self.ws["fused_error"].item())
 
     def max_seqs_estimate(self) -> int:
         return max(self.cfg.max_num_seqs, 16)

@@ -384,30 +384,18 @@ class LlamaModel:
         q = ws["q"][:B]
         attn = ws["attn"][:B]
         act = ws["act"][:B]
-        L0 = self.layers[0]
-        fused_attn = (ws.get("fuse_qkv_attn", False) and ws["part_tokens"] == 256 and
-                      ops.fused_qkv_attention_ok(residual, L0.qkv_ps if L0.qkv_ps is not None
-                                                 else L0.qkv, nq, nkv, k_caches[0],
-                                                 ws["max_parts"], L0.qkv_ps is not None,
-                                                 L0.qkv_s))
         for li, L in enumerate(self.layers):
             ps = L.qkv_ps is not None
             if L.qkv_s is not None and not ps:
                 raise RuntimeError("fp8 decode needs prepare_decode_weights()")
             wq = L.qkv_ps if ps else L.qkv
-            if fused_attn:
-                ops.decode_qkv_attention(residual, wq, eps, md.positions, md.slot_mapping,
-                                         self.cos_sin, k_caches[li], v_caches[li], nq, nkv,
-                                         md.block_tables, md.seq_kvlen, self.scale, ws, q, attn,
-                                         w_scale=L.qkv_s)
-            else:
-                ops.decode_qkv_rope(residual, wq, eps, md.positions, md.slot_mapping, self.cos_sin,
-                                    k_caches[li], v_caches[li], nq, nkv, q_out=q, preshuffled=ps,
-                                    w_scale=L.qkv_s)
-                ops.attention_decode_v2(q, k_caches[li], v_caches[li], md.block_tables,
-                                        md.seq_kvlen, md.seq_qstart, self.scale, ws["part_out"],
-                                        ws["part_lse"], ws["counters"], ws["max_parts"],
-                                        ws["part_tokens"], out=attn, num_seqs=B)
+            ops.decode_qkv_rope(residual, wq, eps, md.positions, md.slot_mapping, self.cos_sin,
+                                k_caches[li], v_caches[li], nq, nkv, q_out=q, preshuffled=ps,
+                                w_scale=L.qkv_s)
+            ops.attention_decode_v2(q, k_caches[li], v_caches[li], md.block_tables,
+                                    md.seq_kvlen, md.seq_qstart, self.scale, ws["part_out"],
+                                    ws["part_lse"], ws["counters"], ws["max_parts"],
+                                    ws["part_tokens"], out=attn, num_seqs=B)
             a2 = attn.view(B, nq * self.head_dim)
             if self.tp_size == 1:
                 ops.linear(a2, L.o_ps if ps else L.o, residual=residual,

@@ -501,34 +501,6 @@ def decode_qkv_rope(x, w, eps, positions, slots, cos_sin, k_cache, v_cache, n_q_
     return q_out
 
 
-def fused_qkv_attention_ok(x, w, n_q_heads, n_kv_heads, k_cache, max_parts, preshuffled,
-                           w_scale=None) -> bool:
-    """Shapes the fused qkv + decode-attention launch supports."""
-    g = n_q_heads // n_kv_heads
-    step = 256 if w_scale is not None else 128
-    return (x.is_cuda and (preshuffled or w_scale is not None) and 1 <= x.shape[0] <= 32
-            and x.shape[1] % step == 0 and n_q_heads % n_kv_heads == 0 and g in (1, 2, 3, 4, 8)
-            and 1 <= max_parts <= 64 and k_cache.shape[2] >= 16)
-
-
-def decode_qkv_attention(x, w, eps, positions, slots, cos_sin, k_cache, v_cache, n_q_heads,
-                         n_kv_heads, block_tables, seq_kvlen, scale, ws, q_out, attn_out,
-                         w_scale=None, wg_trace=None):
-    """RMSNorm(x) -> QKV GEMV -> RoPE -> paged KV write AND the decode attention of the same
-    rows in ONE launch (ops/csrc/attention_decode.hip qkv_attn_kernel): the attention
-    workgroups load the cached context while the qkv workgroups stream the weights, then take
-    q and the new token's k / v straight from them.  ``ws`` holds the split-K partials and the
-    hand-off words (ModelRunner.ws); 256-token partitions, ``ws["max_parts"]`` of them.
-    ``wg_trace`` (int64 [4 * workgroups]): per-workgroup [start, past-wait, end, CU id]
-    timeline on the 100 MHz wall clock (scripts/gpu/trace_fused_qkv_attn.py)."""
-    _native().fused_qkv_attn(q_out, k_cache, v_cache, x, w, positions, slots, cos_sin, n_q_heads,
-                             n_kv_heads, eps, attn_out, ws["part_out"], ws["part_lse"],
-                             ws["counters"], block_tables, seq_kvlen, ws["max_parts"], scale,
-                             ws["side_kv"], ws["pub_counters"], ws["exit_counters"],
-                             ws["fused_error"], w_scale, wg_trace)
-    return attn_out
-
-
 def decode_gate_up_silu(x, w, eps, out=None, preshuffled=False, w_scale=None, ksplit=None):
     """RMSNorm(x) -> gate_up GEMM -> SiLU(gate) * up, one kernel on the GPU."""
     _need_cuda(x, preshuffled or w_scale is not None)

@@ -19,10 +19,6 @@
 // bf16 output, then re-arms the counter (counters are zeroed once at allocation).
 #include "common.h"
 #include "kernels.h"
-#include "skinny.h"
-
-#include <algorithm>
-#include <cstdlib>
 
 namespace atta {
 namespace dec {
@@ -68,18 +64,8 @@ struct DecParams {
   int64_t q_stride, out_stride;
   int bt_stride, n_kv_heads, bs_shift, part_tokens, max_parts;
   float scale_log2;
-  // fused qkv + attention launch (qkv_attn.hip): the q rows and the new token's k / v rows
-  // arrive from the launch's qkv workgroups (write-through) - wait on pub_counters[hk] for
-  // pub_target arrivals, then read them with device-scope loads; every attention workgroup
-  // then arrives on exit_counters[hk] and the last of wgs_per_hk re-arms both counters
-  const uint16_t* side_kv;  // [S][Hkv][2][128]
-  int* pub_counters;
-  int* exit_counters;
-  int pub_target, wgs_per_hk;
-  int* error_word;          // bit 0: a wait timed out (results are garbage, host raises)
   // optional per-workgroup timeline (100 MHz wall clock): [start, past-wait, end, hw id]
   unsigned long long* wg_trace;
-  int poll_sleeps;          // consumer poll interval, ~0.27 us units (ATTA_FUSED_POLL_SLEEPS)
 };
 
 template <typename T>
@@ -88,38 +74,7 @@ struct TileFrags {
   i16x4 v[8];
 };
 
-// Device-scope relaxed poll of one counter (one lane), bounded: ~1 s, then the error word.
-__device__ __forceinline__ void wait_count(int* ctr, int target, int* err, int sleeps = 1) {
-  uint32_t spins = 0;
-  // sparse polls (sleeps x ~0.27 us apart): pollers hammering the counter lines slow the
-  // weight stream of the producers they wait for (MI355X_MICROARCH.md polling-cost)
-  while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-    for (int i = 0; i < sleeps; ++i) __builtin_amdgcn_s_sleep(10);
-    if (++spins > (1u << 20)) {
-      __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
-  }
-}
-
-// Fused mode: this workgroup is done with the launch's hand-off words; the last of the KV
-// head's attention workgroups re-arms them for the next launch.  Every poller of the head has
-// passed its wait by then; the last one still waits for all producers itself, since a launch
-// may have no poller for a head at all (graph-capture warm-up over dummy rows) and a
-// producer arriving after the reset would leave the next launch's count ahead.
-__device__ __forceinline__ void fused_exit(const DecParams& p, int hk) {
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(p.exit_counters + hk, 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-    if (old == p.wgs_per_hk - 1) {
-      wait_count(p.pub_counters + hk, p.pub_target, p.error_word);
-      __hip_atomic_store(p.pub_counters + hk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(p.exit_counters + hk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-template <typename T, int G, int WAVES, int TPW, bool FUSED>
+template <typename T, int G, int WAVES, int TPW>
 __device__ __forceinline__ void decode_attention_body(const DecParams& p, const int s,
                                                       const int hk, const int part,
                                                       unsigned long long (&tr)[3]) {
@@ -147,33 +102,26 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
     bte[i] = bt[min(kt[i] >> p.bs_shift, p.bt_stride - 1)];
   }
   int kvlen = p.seq_kvlen[s];
-  // decode rows are in sequence order in the fused path (one token per sequence)
-  int qrow = FUSED ? s : p.seq_qstart[s + 1] - 1;
+  int qrow = p.seq_qstart[s + 1] - 1;
   // one wait for all of them (keeps the compiler from chaining the loads behind branches)
   asm volatile("" : "+s"(kvlen), "+s"(qrow));
 #pragma unroll
   for (int i = 0; i < TPW; ++i) asm volatile("" : "+s"(bte[i]));
-  // timeline probe (fused launch): clock reads only after the scalar loads above - an
-  // earlier one makes them vector loads, which the scalar-operand asm cannot take
+  // timeline probe: clock reads only after the scalar loads above - an earlier one makes
+  // them vector loads, which the scalar-operand asm cannot take
   tr[0] = wall_clock64();
   const int nparts = (kvlen + PT - 1) / PT;
-  if (part >= nparts) {  // block-uniform (also kvlen == 0 dummy sequences)
-    if constexpr (FUSED) fused_exit(p, hk);
-    return;
-  }
+  if (part >= nparts) return;  // block-uniform (also kvlen == 0 dummy sequences)
   const int kv_end = min(kvlen, kv_begin + PT);
-  // fused: the newest token's k / v come from this launch's qkv workgroups, not the cache
-  const int kv_end_cache = FUSED ? min(kv_end, kvlen - 1) : kv_end;
-  const bool new_part = FUSED && kv_end == kvlen;  // this partition owns the newest token
   const int BS = 1 << p.bs_shift;
   const int64_t hs = static_cast<int64_t>(BS) * kD;
   int page[TPW];
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) page[i] = kt[i] < kv_end_cache ? bte[i] : 0;
+  for (int i = 0; i < TPW; ++i) page[i] = kt[i] < kv_end ? bte[i] : 0;
 
   // ---- round trip 2: Q fragment (needs the query row) + K/V fragments of all tiles --------
   frag8 qf[4];
-  if constexpr (!FUSED) {
+  {
     const bool ok = col < G;
     const uint16_t* qp = p.q + static_cast<int64_t>(qrow) * p.q_stride +
                          static_cast<int64_t>(hk * G + (ok ? col : 0)) * kD + 32 * grp;
@@ -185,7 +133,7 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
   TileFrags<T> f[TPW];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
-    if (kt[i] < kv_end_cache) {
+    if (kt[i] < kv_end) {
       const uint16_t* base = p.k_cache + (static_cast<int64_t>(page[i]) * p.n_kv_heads + hk) * hs;
       const uint16_t* kp = base + static_cast<int64_t>((kt[i] + col) & (BS - 1)) * kD + 32 * grp;
 #pragma unroll
@@ -198,62 +146,17 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
     }
   }
 
-  TileFrags<T> fn;  // fused: the newest token as a one-row tile (wave 0 of new_part)
-  if constexpr (FUSED) {
-    // the cache tiles above are in flight; now wait for this KV head's q / k / v producers
-    if (threadIdx.x == 0) wait_count(p.pub_counters + hk, p.pub_target, p.error_word, p.poll_sleeps);
-    __syncthreads();
-    tr[1] = wall_clock64();  // timeline probe (stored at exit)
-    // device-scope loads of the handed-off rows (written 16 B write-through by producers)
-    const bool ok = col < G;
-    const auto rq = dev_rsrc(p.q);
-    const uint32_t qoff = static_cast<uint32_t>(
-        (static_cast<int64_t>(qrow) * p.q_stride + (hk * G + (ok ? col : 0)) * kD + 32 * grp) * 2);
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-      qf[kk] = ok ? __builtin_bit_cast(frag8, dev_load16(rq, qoff + 16 * kk)) : frag8{};
-    if (new_part && wid == 0) {
-      const auto rs = dev_rsrc(p.side_kv);
-      const uint32_t kb = static_cast<uint32_t>(((s * p.n_kv_heads + hk) * 2) * kD * 2);
-      // K^T operand: row (l & 15) = token 0 only
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
-        fn.k[kk] = col == 0 ? __builtin_bit_cast(frag8, dev_load16(rs, kb + (32 * grp + 8 * kk) * 2))
-                            : frag8{};
-      // V^T operand: lane holds d = 16 dt + col, tokens 4 grp .. +3 -> token 0 in grp 0
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) {
-        i16x4 v = {0, 0, 0, 0};
-        if (grp == 0) {
-          const int d = 16 * dt + col;
-          const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(
-              rs, kb + (kD + (d & ~1)) * 2, 0, kScDevice);
-          v[0] = static_cast<short>((d & 1) ? (w >> 16) : (w & 0xFFFF));
-        }
-        fn.v[dt] = v;
-      }
-    }
-  }
-
   // ---- compute --------------------------------------------------------------------------
   f32x4 o[8];
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_run = kNegInf, l_run = 0.f;
-  // FUSED adds one pass (i == TPW) over the newest-token tile on wave 0 of new_part
-  constexpr int NT = FUSED ? TPW + 1 : TPW;
 #pragma unroll
-  for (int i = 0; i < NT; ++i) {
-    const bool extra = FUSED && i == TPW;
-    if (extra) {
-      if (!(new_part && wid == 0)) break;  // wave-uniform
-    } else if (kt[i] >= kv_end_cache) {
-      if constexpr (FUSED) continue;  // the newest-token pass may still follow
-      else break;                     // wave-uniform
-    }
-    const TileFrags<T>& ft = extra ? fn : f[FUSED ? (i < TPW ? i : 0) : i];
-    const int kbase = extra ? kvlen - 1 : kt[i < TPW ? i : 0];
-    const int kend = extra ? kvlen : kv_end_cache;
+  for (int i = 0; i < TPW; ++i) {
+    if (kt[i] >= kv_end) break;  // wave-uniform
+    const TileFrags<T>& ft = f[i];
+    const int kbase = kt[i];
+    const int kend = kv_end;
     f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) sacc = Mf<T>::qk(ft.k[kk], qf[kk], sacc);
@@ -286,8 +189,7 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
       o[dt] = Mf<T>::pv(ft.v[dt], pf, o[dt]);
     }
   }
-  if constexpr (FUSED) fused_exit(p, hk);  // past its wait: the hand-off words may re-arm
-  else tr[1] = wall_clock64();
+  tr[1] = wall_clock64();
 
   // ---- merge the WAVES partial states (only the G valid columns) ---------------------------
   if (col < G) {
@@ -440,7 +342,7 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
 template <typename T, int G, int WAVES, int TPW>
 __global__ __launch_bounds__(WAVES * 64) void decode_attention_kernel(DecParams p) {
   unsigned long long tr[3] = {0, 0, 0};
-  decode_attention_body<T, G, WAVES, TPW, false>(p, blockIdx.x, blockIdx.y, blockIdx.z, tr);
+  decode_attention_body<T, G, WAVES, TPW>(p, blockIdx.x, blockIdx.y, blockIdx.z, tr);
   // timeline probe (set_attention_trace): [past round trip 1, computed, published, end]
   if (p.wg_trace != nullptr && threadIdx.x == 0) {
     const int64_t b = blockIdx.x + static_cast<int64_t>(gridDim.x) *
@@ -474,67 +376,6 @@ static int launch(int G, int part_tokens, dim3 grid, hipStream_t st, const DecPa
     case 512: return launch_g<T, 16, 2>(G, grid, st, p);
     default: return -1;
   }
-}
-
-// ---- fused qkv projection + decode attention (one launch per layer) ----------------------
-// EXPERIMENT, off by default (EngineConfig.fuse_qkv_attn): measured 29-30 us per layer vs
-// 20.4 us for the two separate launches (profiles/r2_fused_qkv_attn_experiment.txt).
-// Workgroups [0, n_tiles) are the qkv+RoPE GEMV tiles (EPI_QKVPUB: q rows and the new
-// token's k / v rows stored write-through, one arrival per tile on its KV head's counter);
-// the rest are decode-attention partitions that issue their cache-tile loads at once, then
-// wait for their KV head's G * 8 + 16 producer tiles and consume the handed-off rows with
-// device-scope loads.  The attention's dependent round trips for the cached context thus run
-// under the qkv weight stream instead of after a kernel boundary.  Producers precede
-// consumers in the grid, so with in-order dispatch a spinning consumer never holds a slot a
-// producer still needs; every wait is bounded regardless (error word, never a hang).
-template <typename T, int G, int MT, bool W8>
-__global__ __launch_bounds__(256) void qkv_attn_kernel(SkinnyParams sp, DecParams dp,
-                                                       int n_tiles, int att_parts) {
-  const int b = blockIdx.x;
-  // timeline probe: every store at the exit - a store ahead of the bodies' loads would let
-  // them alias it and demote their scalar loads to vector ones
-  unsigned long long t0 = 0, t_wait = 0;
-  unsigned long long tr[3] = {0, 0, 0};
-  if (b < n_tiles) {
-    t0 = wall_clock64();
-    skinny_body<T, 4, W8 ? 8 : 4, MT, EPI_QKVPUB, true, true, W8>(sp, b, 0);
-  } else {
-    const int a = b - n_tiles;
-    const int part = a % att_parts;
-    const int hk = (a / att_parts) % dp.n_kv_heads;
-    const int s = a / (att_parts * dp.n_kv_heads);
-    decode_attention_body<T, G, 4, 4, true>(dp, s, hk, part, tr);
-    t0 = tr[0];
-    t_wait = tr[1];
-  }
-  if (dp.wg_trace != nullptr && threadIdx.x == 0) {
-    dp.wg_trace[4 * b] = t0;
-    dp.wg_trace[4 * b + 1] = t_wait;
-    dp.wg_trace[4 * b + 2] = wall_clock64();
-    dp.wg_trace[4 * b + 3] = __smid();
-  }
-}
-
-template <typename T, int MT, bool W8>
-static int launch_fused_g(int G, dim3 grid, hipStream_t st, const SkinnyParams& sp,
-                          const DecParams& dp, int n_tiles, int parts) {
-  switch (G) {
-    case 1: qkv_attn_kernel<T, 1, MT, W8><<<grid, 256, 0, st>>>(sp, dp, n_tiles, parts); return 0;
-    case 2: qkv_attn_kernel<T, 2, MT, W8><<<grid, 256, 0, st>>>(sp, dp, n_tiles, parts); return 0;
-    case 3: qkv_attn_kernel<T, 3, MT, W8><<<grid, 256, 0, st>>>(sp, dp, n_tiles, parts); return 0;
-    case 4: qkv_attn_kernel<T, 4, MT, W8><<<grid, 256, 0, st>>>(sp, dp, n_tiles, parts); return 0;
-    case 8: qkv_attn_kernel<T, 8, MT, W8><<<grid, 256, 0, st>>>(sp, dp, n_tiles, parts); return 0;
-    default: return -1;
-  }
-}
-
-template <typename T>
-static int launch_fused(int G, int mt, bool w8, dim3 grid, hipStream_t st, const SkinnyParams& sp,
-                        const DecParams& dp, int n_tiles, int parts) {
-  if (w8) return mt == 1 ? launch_fused_g<T, 1, true>(G, grid, st, sp, dp, n_tiles, parts)
-                         : launch_fused_g<T, 2, true>(G, grid, st, sp, dp, n_tiles, parts);
-  return mt == 1 ? launch_fused_g<T, 1, false>(G, grid, st, sp, dp, n_tiles, parts)
-                 : launch_fused_g<T, 2, false>(G, grid, st, sp, dp, n_tiles, parts);
 }
 
 }  // namespace dec
@@ -586,89 +427,6 @@ int atta_attention_decode_v2(void* out, float* part_out, float* part_lse, int* c
   dim3 grid(num_seqs, n_kv_heads, max_parts);
   const int rc = dtype == 0 ? dec::launch<__bf16>(G, part_tokens, grid, stream, p)
                             : dec::launch<_Float16>(G, part_tokens, grid, stream, p);
-  if (rc) return rc;
-  return static_cast<int>(hipGetLastError());
-}
-
-int atta_fused_qkv_attn(void* q_out, void* k_cache, void* v_cache, const void* x, const void* w,
-                        const int* positions, const int* slots, const float* cos_sin, int M,
-                        int K, int64_t x_stride, int n_q_heads, int n_kv_heads, int block_size,
-                        float eps, const float* wscale, void* out, float* part_out,
-                        float* part_lse, int* counters, const int* block_tables,
-                        const int* seq_kvlen, int max_parts, int bt_stride, float scale,
-                        void* side_kv, int* pub_counters, int* exit_counters, int* error_word,
-                        unsigned long long* wg_trace, int dtype, hipStream_t stream) {
-  const int G = n_q_heads / n_kv_heads;
-  int shift = 0;
-  while ((1 << shift) < block_size) ++shift;
-  if ((1 << shift) != block_size || block_size < 16) return -1;
-  if (n_q_heads % n_kv_heads || G > 8 || ((G & (G - 1)) && G != 3)) return -1;
-  if (M < 1 || M > 32 || max_parts < 1 || max_parts > 64) return -1;
-  const bool w8 = wscale != nullptr;
-  if (K % ((w8 ? 64 : 32) * 4) != 0) return -1;  // 4 waves, whole MFMA K-steps
-  SkinnyParams sp{};
-  sp.ps = 1;
-  sp.wscale = wscale;
-  sp.x = static_cast<const uint16_t*>(x);
-  sp.w = static_cast<const uint16_t*>(w);
-  sp.y = static_cast<uint16_t*>(q_out);
-  sp.x_stride = x_stride;
-  sp.y_stride = static_cast<int64_t>(n_q_heads) * 128;
-  sp.M = M;
-  sp.K = K;
-  sp.N = (n_q_heads + 2 * n_kv_heads) * 128;
-  sp.eps = eps;
-  sp.k_cache = static_cast<uint16_t*>(k_cache);
-  sp.v_cache = static_cast<uint16_t*>(v_cache);
-  sp.positions = positions;
-  sp.slots = slots;
-  sp.cos_sin = cos_sin;
-  sp.n_q_heads = n_q_heads;
-  sp.n_kv_heads = n_kv_heads;
-  sp.bs_shift = shift;
-  sp.ksplit = 1;
-  sp.side_kv = static_cast<uint16_t*>(side_kv);
-  sp.pub_counters = pub_counters;
-  dec::DecParams dp{};
-  dp.out = static_cast<uint16_t*>(out);
-  dp.part_out = part_out;
-  dp.part_lse = part_lse;
-  dp.counters = counters;
-  dp.q = static_cast<const uint16_t*>(q_out);
-  dp.k_cache = static_cast<const uint16_t*>(k_cache);
-  dp.v_cache = static_cast<const uint16_t*>(v_cache);
-  dp.block_tables = block_tables;
-  dp.seq_kvlen = seq_kvlen;
-  dp.seq_qstart = nullptr;
-  dp.q_stride = sp.y_stride;
-  dp.out_stride = sp.y_stride;
-  dp.bt_stride = bt_stride;
-  dp.n_kv_heads = n_kv_heads;
-  dp.bs_shift = shift;
-  dp.part_tokens = 256;
-  dp.max_parts = max_parts;
-  dp.scale_log2 = scale * 1.4426950408889634f;
-  dp.side_kv = static_cast<const uint16_t*>(side_kv);
-  dp.pub_counters = pub_counters;
-  dp.exit_counters = exit_counters;
-  dp.pub_target = G * 8 + 16;
-  dp.wgs_per_hk = M * max_parts;
-  dp.error_word = error_word;
-  dp.wg_trace = wg_trace;
-  static const int poll_sleeps = [] {
-    const char* e = getenv("ATTA_FUSED_POLL_SLEEPS");
-    return e ? std::max(1, atoi(e)) : 1;
-  }();
-  dp.poll_sleeps = poll_sleeps;
-  const int n_tiles = sp.N / 16;
-  // timing probe only (scripts/gpu/trace_fused_qkv_attn.py): the producer tiles alone - the
-  // hand-off counters are left armed, so results of later launches are garbage
-  static const bool producers_only = getenv("ATTA_FUSED_PRODUCERS_ONLY") != nullptr;
-  dim3 grid(n_tiles + (producers_only ? 0 : M * n_kv_heads * max_parts));
-  const int mt = M <= 16 ? 1 : 2;
-  const int rc = dtype == 0
-                     ? dec::launch_fused<__bf16>(G, mt, w8, grid, stream, sp, dp, n_tiles, max_parts)
-                     : dec::launch_fused<_Float16>(G, mt, w8, grid, stream, sp, dp, n_tiles, max_parts);
   if (rc) return rc;
   return static_cast<int>(hipGetLastError());
 }

@@ -472,63 +472,6 @@ void set_attention_trace(const c10::optional<at::Tensor>& trace) {
   }
 }
 
-void fused_qkv_attn(at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache, const at::Tensor& x,
-                    const at::Tensor& w, const at::Tensor& positions, const at::Tensor& slots,
-                    const at::Tensor& cos_sin, int64_t n_q_heads, int64_t n_kv_heads, double eps,
-                    at::Tensor out, at::Tensor part_out, at::Tensor part_lse, at::Tensor counters,
-                    const at::Tensor& block_tables, const at::Tensor& seq_kvlen, int64_t max_parts,
-                    double scale, at::Tensor side_kv, at::Tensor pub_counters,
-                    at::Tensor exit_counters, at::Tensor error_word,
-                    const c10::optional<at::Tensor>& w_scale,
-                    const c10::optional<at::Tensor>& wg_trace) {
-  check_skinny(x, w, "fused_qkv_attn");
-  const float* ws = fp8_scale(w, w_scale, "fused_qkv_attn");
-  const int64_t M = x.size(0);
-  TORCH_CHECK(w.size(0) == (n_q_heads + 2 * n_kv_heads) * 128, "fused_qkv_attn: w rows");
-  TORCH_CHECK(positions.scalar_type() == at::kInt && slots.scalar_type() == at::kInt &&
-                  block_tables.scalar_type() == at::kInt && seq_kvlen.scalar_type() == at::kInt &&
-                  counters.scalar_type() == at::kInt && pub_counters.scalar_type() == at::kInt &&
-                  exit_counters.scalar_type() == at::kInt && error_word.scalar_type() == at::kInt,
-              "fused_qkv_attn: int32 metadata / counters");
-  TORCH_CHECK(positions.numel() >= M && slots.numel() >= M && seq_kvlen.numel() >= M &&
-                  block_tables.size(0) >= M,
-              "fused_qkv_attn: metadata rows");
-  TORCH_CHECK(q_out.is_contiguous() && q_out.numel() >= M * n_q_heads * 128 &&
-                  out.is_contiguous() && out.numel() >= M * n_q_heads * 128 &&
-                  q_out.scalar_type() == x.scalar_type() && out.scalar_type() == x.scalar_type(),
-              "fused_qkv_attn: q / out [M, Hq, 128] contiguous");
-  TORCH_CHECK(k_cache.size(1) == n_kv_heads && k_cache.size(3) == 128 && v_cache.size(2) == 128,
-              "fused_qkv_attn: caches");
-  TORCH_CHECK(side_kv.numel() >= M * n_kv_heads * 2 * 128 && side_kv.scalar_type() == x.scalar_type(),
-              "fused_qkv_attn: side_kv [M, Hkv, 2, 128]");
-  TORCH_CHECK(pub_counters.numel() >= n_kv_heads && exit_counters.numel() >= n_kv_heads &&
-                  counters.numel() >= M * n_kv_heads && error_word.numel() >= 1,
-              "fused_qkv_attn: counters");
-  TORCH_CHECK(part_out.numel() >= M * n_kv_heads * max_parts * 16 * 128 &&
-                  part_lse.numel() >= M * n_kv_heads * max_parts * 16,
-              "fused_qkv_attn: split-K workspace");
-  unsigned long long* trace_ptr = nullptr;
-  if (wg_trace.has_value()) {
-    const int64_t wgs = (n_q_heads + 2 * n_kv_heads) * 8 + M * n_kv_heads * max_parts;
-    TORCH_CHECK(wg_trace->scalar_type() == at::kLong && wg_trace->is_contiguous() &&
-                    wg_trace->numel() >= 4 * wgs,
-                "fused_qkv_attn: wg_trace int64 [", 4 * wgs, "]");
-    trace_ptr = reinterpret_cast<unsigned long long*>(wg_trace->data_ptr<int64_t>());
-  }
-  const at::DeviceGuard g(x.device());
-  check_rc(atta_fused_qkv_attn(
-               q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), x.data_ptr(), w.data_ptr(),
-               positions.data_ptr<int>(), slots.data_ptr<int>(), cos_sin.data_ptr<float>(), M,
-               x.size(1), x.stride(0), n_q_heads, n_kv_heads, k_cache.size(2),
-               static_cast<float>(eps), ws, out.data_ptr(), part_out.data_ptr<float>(),
-               part_lse.data_ptr<float>(), counters.data_ptr<int>(), block_tables.data_ptr<int>(),
-               seq_kvlen.data_ptr<int>(), max_parts, block_tables.stride(0),
-               static_cast<float>(scale), side_kv.data_ptr(), pub_counters.data_ptr<int>(),
-               exit_counters.data_ptr<int>(), error_word.data_ptr<int>(), trace_ptr, dtype_code(x),
-               cur_stream()),
-           "fused_qkv_attn");
-}
-
 void skinny_variant(at::Tensor y, const at::Tensor& x, const at::Tensor& w, int64_t variant) {
   check_skinny(x, w, "skinny_variant");
   TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.scalar_type() == at::kBFloat16,
@@ -650,13 +593,6 @@ TORCH_LIBRARY(atta, m) {
   m.def("fused_gate_up_silu(Tensor(a!) out, Tensor x, Tensor w, float eps, int waves, "
         "bool preshuffled=False, Tensor? w_scale=None, int ksplit=1) -> ()");
   m.def("set_splitk_workspace(Tensor ws, Tensor counters) -> ()");
-  m.def(
-      "fused_qkv_attn(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor x, "
-      "Tensor w, Tensor positions, Tensor slots, Tensor cos_sin, int n_q_heads, int n_kv_heads, "
-      "float eps, Tensor(d!) out, Tensor(e!) part_out, Tensor(f!) part_lse, Tensor(g!) counters, "
-      "Tensor block_tables, Tensor seq_kvlen, int max_parts, float scale, Tensor(h!) side_kv, "
-      "Tensor(i!) pub_counters, Tensor(j!) exit_counters, Tensor(k!) error_word, "
-      "Tensor? w_scale=None, Tensor(l!)? wg_trace=None) -> ()");
   m.def("quant_rows_fp8(Tensor(a!) q, Tensor(b!) scale, Tensor x, Tensor? w, int mode, "
         "float eps, Tensor(c!)? residual=None) -> ()");
   m.def(
@@ -711,7 +647,6 @@ TORCH_LIBRARY_IMPL(atta, CUDA, m) {
   m.impl("fused_lm_head_sample", &fused_lm_head_sample);
   m.impl("sample_finalize", &sample_finalize);
   m.impl("set_splitk_workspace", &set_splitk_workspace);
-  m.impl("fused_qkv_attn", &fused_qkv_attn);
   m.impl("quant_rows_fp8", &quant_rows_fp8);
   m.impl("attention_decode_v2", &attention_decode_v2);
   m.impl("skinny_variant", &skinny_variant);

@@ -122,13 +122,3 @@ int64_t atta_ar2_error_offset();
 int atta_ar2_run(void* const* bases, int rank, int world, int64_t max_elems, const void* x,
                  void* y, int64_t n, int dtype, hipStream_t stream);
 
-// Fused qkv(+norm+RoPE+KV write) GEMV and decode attention in one launch (attention_decode.hip);
-// pre-shuffled weights (16-bit or fp8 with wscale), 256-token partitions, <= 64 partitions.
-int atta_fused_qkv_attn(void* q_out, void* k_cache, void* v_cache, const void* x, const void* w,
-                        const int* positions, const int* slots, const float* cos_sin, int M,
-                        int K, int64_t x_stride, int n_q_heads, int n_kv_heads, int block_size,
-                        float eps, const float* wscale, void* out, float* part_out,
-                        float* part_lse, int* counters, const int* block_tables,
-                        const int* seq_kvlen, int max_parts, int bt_stride, float scale,
-                        void* side_kv, int* pub_counters, int* exit_counters, int* error_word,
-                        unsigned long long* wg_trace, int dtype, hipStream_t stream);

@@ -1,5 +1,7 @@
-// Skinny (decode) GEMM body shared by the GEMV kernels (gemv.hip) and the fused
-// qkv + decode-attention launch (qkv_attn.hip).  See gemv.hip for the design notes.
+// Skinny (decode) GEMM body of the GEMV kernels (gemv.hip: launchers and design notes),
+// one 16-output-row tile per call - kept in a header so a persistent or fused launch can
+// reuse it (the fused qkv + attention launch that did was measured slower and removed:
+// profiles/r2_fused_qkv_attn_experiment.txt).
 #pragma once
 
 #include "common.h"
@@ -11,11 +13,7 @@ enum Epi {
   EPI_RESADD = 1,
   EPI_QKVROPE = 2,
   EPI_SILU = 3,
-  EPI_SAMPLE = 4,
-  // QKVROPE for the fused qkv + attention launch (qkv_attn.hip): q rows and the new token's
-  // k / v rows are stored write-through (16-byte sc1) and each tile then arrives on its KV
-  // head's counter, so attention workgroups of the same launch can consume them
-  EPI_QKVPUB = 5
+  EPI_SAMPLE = 4
 };
 
 template <typename T>
@@ -89,9 +87,6 @@ struct SkinnyParams {
   int ksplit;
   float* sk_ws;
   int* sk_counters;
-  // EPI_QKVPUB: new-token k / v rows [M][n_kv_heads][2][128] and per-KV-head arrival counters
-  uint16_t* side_kv;
-  int* pub_counters;
 };
 
 __device__ __forceinline__ unsigned ordered_bits(float f) {
@@ -107,7 +102,7 @@ __device__ __forceinline__ float gumbel_noise(uint64_t seed, uint64_t step, uint
 
 template <int EPI>
 __device__ __forceinline__ int tile_row(int tile, int c, const SkinnyParams& p) {
-  if constexpr (EPI == EPI_QKVROPE || EPI == EPI_QKVPUB) {
+  if constexpr (EPI == EPI_QKVROPE) {
     // head-dim 128: tile = head * 8 + j covers dims {8j..8j+7} and {64+8j..64+8j+7}
     const int head = tile >> 3, j = tile & 7;
     return head * 128 + j * 8 + (c & 7) + ((c & 8) ? 64 : 0);
@@ -378,72 +373,6 @@ __device__ __forceinline__ void skinny_body(const SkinnyParams& p, const int til
         vc[static_cast<int64_t>(d) * BS] = from_f32<T>(x1);
         vc[static_cast<int64_t>(d + 64) * BS] = from_f32<T>(x2);
       }
-    }
-  } else if constexpr (EPI == EPI_QKVPUB) {
-    // one thread per row: the tile's 8 rotated (d, d + 64) pairs -> two 16-byte stores
-    const int head = tile >> 3, jb = (tile & 7) * 8;
-    const int nq = p.n_q_heads, nkv = p.n_kv_heads;
-    const int BS = 1 << p.bs_shift;
-    const int m = threadIdx.x;
-    if (m < p.M) {
-      const float sc = norm ? inv_rms[m] : 1.f;
-      const int slot = p.slots[m];
-      Pack8 lo, hi;
-      if (head < nq + nkv) {
-        const float* cs = p.cos_sin + static_cast<int64_t>(p.positions[m]) * 128;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const float x1 = to_f32<T>(from_f32<T>(red[0][m][c] * sc));
-          const float x2 = to_f32<T>(from_f32<T>(red[0][m][c + 8] * sc));
-          const float co = cs[jb + c], si = cs[64 + jb + c];
-          lo.v[c] = from_f32<T>(x1 * co - x2 * si);
-          hi.v[c] = from_f32<T>(x2 * co + x1 * si);
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          lo.v[c] = from_f32<T>(red[0][m][c] * sc);
-          hi.v[c] = from_f32<T>(red[0][m][c + 8] * sc);
-        }
-      }
-      const u32x4 lo4 = __builtin_bit_cast(u32x4, lo), hi4 = __builtin_bit_cast(u32x4, hi);
-      if (head < nq) {
-        const auto rq = dev_rsrc(p.y);
-        const uint32_t off = static_cast<uint32_t>((m * p.y_stride + head * 128 + jb) * 2);
-        dev_store16(rq, off, lo4);
-        dev_store16(rq, off + 128, hi4);
-      } else {
-        const bool isk = head < nq + nkv;
-        const int hk = isk ? head - nq : head - nq - nkv;
-        const auto rs = dev_rsrc(p.side_kv);
-        const uint32_t off =
-            static_cast<uint32_t>((((m * nkv + hk) * 2 + (isk ? 0 : 1)) * 128 + jb) * 2);
-        dev_store16(rs, off, lo4);
-        dev_store16(rs, off + 128, hi4);
-        if (slot >= 0) {  // the paged cache, for later steps (plain stores)
-          const int64_t pg = static_cast<int64_t>(slot >> p.bs_shift) * nkv + hk;
-          if (isk) {
-            uint16_t* kc = p.k_cache + (pg * BS + (slot & (BS - 1))) * 128;
-            *reinterpret_cast<Pack8*>(kc + jb) = lo;
-            *reinterpret_cast<Pack8*>(kc + 64 + jb) = hi;
-          } else {
-            uint16_t* vc = p.v_cache + pg * 128 * BS + (slot & (BS - 1));
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-              vc[static_cast<int64_t>(jb + c) * BS] = lo.v[c];
-              vc[static_cast<int64_t>(64 + jb + c) * BS] = hi.v[c];
-            }
-          }
-        }
-      }
-    }
-    // R1 publish: every storing wave drains its write-through stores, then one lane arrives
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const int g = nq / nkv;
-      const int hk = head < nq ? head / g : (head < nq + nkv ? head - nq : head - nq - nkv);
-      __hip_atomic_fetch_add(p.pub_counters + hk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   } else if constexpr (EPI == EPI_SAMPLE) {
     // one row per thread group of 16 columns: thread e handles (m, n) and reduces over n

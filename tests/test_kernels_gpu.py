@@ -674,79 +674,3 @@ def test_gemm_fp8_rowwise(m):
         (wq.view(torch.float8_e4m3fn).float() * ws[:, None]).t()
     err = (got.float() - exp).abs().max() / exp.abs().max()
     assert float(err) < 1e-2
-
-
-def _fused_ws(B, hkv, max_parts, dt):
-    return {"part_out": torch.empty(B * hkv * max_parts * 16 * 128, device="cuda"),
-            "part_lse": torch.empty(B * hkv * max_parts * 16, device="cuda"),
-            "counters": torch.zeros(B * hkv, dtype=torch.int32, device="cuda"),
-            "side_kv": torch.zeros(B, hkv, 2, 128, dtype=dt, device="cuda"),
-            "pub_counters": torch.zeros(hkv, dtype=torch.int32, device="cuda"),
-            "exit_counters": torch.zeros(hkv, dtype=torch.int32, device="cuda"),
-            "fused_error": torch.zeros(1, dtype=torch.int32, device="cuda"),
-            "max_parts": max_parts}
-
-
-@pytest.mark.parametrize("fp8", [False, True])
-@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 1), (24, 8)])
-def test_fused_qkv_attention(fp8, hq, hkv):
-    """One launch of qkv(+norm+RoPE+KV write) and decode attention == the two-launch path:
-    q / K / V writes bit-identical, attention within fp32-reordering tolerance of the fp32
-    reference (the newest token is consumed from the producers, not the cache), dummy rows
-    (kvlen 0), partition boundaries, counters re-armed, no wait timed out."""
-    torch.manual_seed(23)
-    dt, H, bs = torch.bfloat16, 4096 if hq <= 32 else 8192, 16
-    ctx = [1, 17, 256, 257, 1000, 3999, 0, 0]  # context BEFORE this token; two dummy rows
-    B = len(ctx)
-    kvlens = [c + 1 if i < 6 else 0 for i, c in enumerate(ctx)]
-    k, v, bt, kvlen, qstart, _ = _make_paged([(max(kv, 1), 1) for kv in kvlens], hkv, bs, dt)
-    kvlen = torch.tensor(kvlens, dtype=torch.int32, device="cuda")
-    pos = torch.tensor([max(kv - 1, 0) for kv in kvlens], dtype=torch.int32, device="cuda")
-    slots = torch.tensor([int(bt[i, (kv - 1) // bs]) * bs + (kv - 1) % bs if kv > 0 else -1
-                          for i, kv in enumerate(kvlens)], dtype=torch.int32, device="cuda")
-    x = torch.randn(B, H, dtype=dt, device="cuda") * 2
-    w = torch.randn((hq + 2 * hkv) * 128, H, dtype=dt, device="cuda") * 0.02
-    cs = ref.rope_cos_sin(128, 8192, 500000.0, None, device="cuda")
-    if fp8:
-        qw, sc = ops.quantize_fp8(w)
-        wp, w_scale = ops.preshuffle_fp8(qw, "qkv"), sc
-    else:
-        wp, w_scale = ops.preshuffle(w, "qkv"), None
-    scale = 1 / math.sqrt(128)
-    max_parts = 16
-    # two-launch path
-    k1, v1 = k.clone(), v.clone()
-    q1 = ops.decode_qkv_rope(x, wp, 1e-5, pos, slots, cs, k1, v1, hq, hkv, preshuffled=True,
-                             w_scale=w_scale)
-    ws1 = _fused_ws(B, hkv, max_parts, dt)
-    a1 = ops.attention_decode_v2(q1, k1, v1, bt, kvlen, qstart, scale, ws1["part_out"],
-                                 ws1["part_lse"], ws1["counters"], max_parts, 256, num_seqs=B)
-    exp = ref.paged_attention(q1, k1, v1, bt.clamp(min=0), kvlen, qstart, scale)
-    ws = _fused_ws(B, hkv, max_parts, dt)
-    # a launch over dummy rows only (graph-capture warm-up: no attention workgroup waits)
-    # must still leave the hand-off words re-armed
-    dummy = torch.zeros_like(kvlen)
-    qd, ad = torch.empty(B, hq, 128, dtype=dt, device="cuda"), torch.empty(B, hq, 128, dtype=dt,
-                                                                             device="cuda")
-    ops.decode_qkv_attention(x, wp, 1e-5, pos, torch.full_like(slots, -1), cs, k.clone(),
-                             v.clone(), hq, hkv, bt, dummy, scale, ws, qd, ad, w_scale=w_scale)
-    torch.cuda.synchronize()
-    assert bool((ws["pub_counters"] == 0).all()) and bool((ws["exit_counters"] == 0).all())
-    for _ in range(3):  # counters must re-arm
-        k2, v2 = k.clone(), v.clone()
-        q2 = torch.full((B, hq, 128), 7.0, dtype=dt, device="cuda")
-        a2 = torch.full((B, hq, 128), 7.0, dtype=dt, device="cuda")
-        ops.decode_qkv_attention(x, wp, 1e-5, pos, slots, cs, k2, v2, hq, hkv, bt, kvlen, scale,
-                                 ws, q2, a2, w_scale=w_scale)
-        torch.cuda.synchronize()
-        assert int(ws["fused_error"][0]) == 0
-        assert bool((ws["pub_counters"] == 0).all()) and bool((ws["exit_counters"] == 0).all())
-        assert bool((ws["counters"] == 0).all())
-        # same products (fp8: the two-launch GEMV splits K over 8 waves, the fused one over
-        # 4); epilogue code differs, so FMA contraction may move a bf16 ulp
-        tol = 2e-2 if fp8 else 8e-3
-        close(q2[:6], q1[:6], tol, tol)
-        close(k2, k1, tol, tol)
-        close(v2, v1, tol, tol)
-        close(a2[:6], exp[:6], 1.5e-2, 2e-2)
-        close(a2[:6], a1[:6], 1e-2, 1e-2)
