@@ -175,14 +175,18 @@ class EngineConfig:
     graph_batch_sizes: tuple = (1, 2, 4, 8, 16, 32, 64, 128, 256)
     # decode split-K partition size (tokens) for the paged attention kernel
     decode_partition_tokens: int = 256
-    # optional finer split for small decode batches (<= decode_small_batch_max sequences).
-    # Off (0): 128-token partitions won in the isolated microbenchmark but lost inside the
-    # real decode step (13.8 vs 12.3 us, profiles/r1_profile_v6_preshuffled.txt)
-    decode_partition_tokens_small: int = 0
+    # finer split for small decode batches (<= decode_small_batch_max sequences): a partition
+    # is one workgroup's K/V stream, and at B <= 8 the attention is bound by per-CU bandwidth
+    # x latency (256 tokens = 128 KB per workgroup, ~2.5 us to land: the timeline of
+    # scripts/gpu/trace_decode_attention.py), so 128-token partitions put twice the CUs on it;
+    # with the one-round-trip merge and partition-bucket graphs this wins in situ (bench
+    # 760.5 -> 765.5 tok/s; r1 measured it losing with the old 4-per-round-trip merge).
+    # Falls back to decode_partition_tokens when max_model_len needs > 64 partitions.
+    decode_partition_tokens_small: int = 128
     # decode hipGraphs per partition bucket (attention grid sized to the step's longest
     # context, not max_model_len); buckets above max_model_len's count are dropped
     graph_parts_buckets: tuple = (1, 2, 4, 6, 8, 12, 16, 24, 32, 48, 64)
-    decode_small_batch_max: int = 2
+    decode_small_batch_max: int = 8
     # chunked prefill: max prompt tokens of one sequence per step (0 = max_num_batched_tokens)
     long_prefill_token_threshold: int = 0
     # fused native decode path (GEMV kernels) when available

@@ -144,6 +144,9 @@ class ModelRunner:
         # (profiles/r2_fused_qkv_attn_experiment.txt: B=8 attention 21.9 us vs 10.8 at B=1)
         self.parts_buckets = sorted({p for p in cfg.graph_parts_buckets if p < self.max_parts}
                                     | {self.max_parts})
+        self.parts_buckets_small = sorted(
+            {p for p in cfg.graph_parts_buckets if p < self.max_parts_small}
+            | {self.max_parts_small})
         self.tile_tokens = ops.prefill_tile_tokens(self.model.g)
         self.graph_sizes = sorted(b for b in cfg.graph_batch_sizes)
         if comm is not None and comm.size > 1 and comm.is_gloo:
@@ -260,8 +263,7 @@ class ModelRunner:
 
     # ------------------------------------------------------------------------------------
     def _ws_for(self, batch_size: int) -> dict:
-        if batch_size <= self.cfg.decode_small_batch_max and \
-                self.part_tokens_small != self.part_tokens:
+        if self._small(batch_size):
             return {**self.ws, "part_tokens": self.part_tokens_small,
                     "max_parts": self.max_parts_small}
         return self.ws
@@ -329,10 +331,19 @@ class ModelRunner:
                         tile_qoff=v["tile_qoff"], logits_idx=v["logits_idx"],
                         num_decode=num_decode, num_tiles=num_tiles)
 
-    def parts_bucket(self, max_kv: int) -> int:
-        """Smallest partition bucket covering a decode step whose longest context is max_kv."""
-        need = max(1, math.ceil(max_kv / self.part_tokens))
-        return next((p for p in self.parts_buckets if p >= need), self.max_parts)
+    def _small(self, batch_size: int) -> bool:
+        return (0 < batch_size <= self.cfg.decode_small_batch_max
+                and self.part_tokens_small != self.part_tokens)
+
+    def parts_bucket(self, max_kv: int, batch_size: int = 0) -> int:
+        """Smallest partition bucket covering a decode step of ``batch_size`` rows whose
+        longest context is max_kv (in the partition size that batch size uses)."""
+        if self._small(batch_size):
+            pt, buckets, top = self.part_tokens_small, self.parts_buckets_small, self.max_parts_small
+        else:
+            pt, buckets, top = self.part_tokens, self.parts_buckets, self.max_parts
+        need = max(1, math.ceil(max_kv / pt))
+        return next((p for p in buckets if p >= need), top)
 
     def _forward_sample(self, v: dict, md: AttnMeta, num_parts: int, special: bool = False):
         """One step's forward + sampling; ``special``: some row uses top-p / top-k (logits
@@ -342,9 +353,9 @@ class ModelRunner:
         if (self.fused_decode and md.num_tiles == 0
                 and md.num_decode == T and m.decode_fusable(T)):
             ws = self._ws_for(T)
-            if ws["part_tokens"] == self.part_tokens:
-                # grid over this step's partition bucket only (num_parts covers every row)
-                ws = {**ws, "max_parts": min(num_parts, self.max_parts)}
+            # grid over this step's partition bucket only (num_parts covers every row, in
+            # the partition size of this batch size: parts_bucket)
+            ws = {**ws, "max_parts": min(num_parts, ws["max_parts"])}
             return m.forward_decode(v["input_ids"], md, self.k_layers, self.v_layers,
                                     ws, v["temperature"], v["seeds"], v["steps"],
                                     prev_tokens=self.ws["tokens"], feed_prev=v["feed_prev"],
@@ -388,7 +399,12 @@ class ModelRunner:
         special = self._special(batch)
         lay, arrays = self._prepare(batch)
         max_kv = int(arrays["seq_kvlen"][:batch.num_decode].max()) if batch.num_decode else 0
-        num_parts = max(1, math.ceil(max_kv / self.part_tokens))
+        if batch.num_decode == n and lay.NT == 0:
+            # decode-only: in the partition size of this batch size (>= the 256-token count
+            # the unfused path needs, within the allocated partials)
+            num_parts = self.parts_bucket(max_kv, n)
+        else:
+            num_parts = max(1, math.ceil(max_kv / self.part_tokens))
         host = self._pack(lay, arrays)
         hdr = np.array([OP_STEP, lay.T, lay.S, lay.W, lay.NT, batch.num_decode, num_parts,
                         0, int(special), n, lay.size, 0], dtype=np.int32)
@@ -418,15 +434,14 @@ class ModelRunner:
         t0 = time.perf_counter()
         if bucket:
             lay, arrays = self._prepare(batch, pad_seqs=bucket, tiles=False)
-            num_parts = self.parts_bucket(int(arrays["seq_kvlen"][:n].max()))
+            num_parts = self.parts_bucket(int(arrays["seq_kvlen"][:n].max()), bucket)
             if (bucket, num_parts, special) not in self.graphs:
                 self.capture(bucket, num_parts, bool(special))
                 t0 = time.perf_counter()
             assert lay.size == self.graph_io[(bucket, num_parts, special)]["layout"].size
         else:
             lay, arrays = self._prepare(batch, tiles=False)
-            max_kv = int(arrays["seq_kvlen"][:n].max())
-            num_parts = max(1, math.ceil(max_kv / self.part_tokens))
+            num_parts = self.parts_bucket(int(arrays["seq_kvlen"][:n].max()), n)
         arrays["feed_prev"] = np.array([1 if lookahead else 0], dtype=np.int32)
         host = self._pack(lay, arrays)
         hdr = np.array([OP_STEP, lay.T, lay.S, lay.W, lay.NT, batch.num_decode, num_parts,
@@ -547,7 +562,7 @@ class ModelRunner:
         """Capture a decode step for `bucket` sequences whose contexts fit `parts` attention
         partitions (default: max_model_len) into a hipGraph; ``special``: the top-k / top-p
         sampler variant (logits materialised)."""
-        parts = parts or self.max_parts
+        parts = parts or (self.max_parts_small if self._small(bucket) else self.max_parts)
         if self.publisher is not None:
             hdr = np.zeros(HDR_WORDS, dtype=np.int32)
             hdr[0], hdr[1], hdr[2], hdr[3] = OP_CAPTURE, bucket, parts, int(special)
@@ -587,7 +602,10 @@ class ModelRunner:
         if not (self.is_cuda and self.cfg.use_graphs):
             return
         for b in self.graph_sizes:
-            for p in (self.parts_buckets if all_parts else [self.max_parts]):
+            small = self._small(b)
+            top = self.max_parts_small if small else self.max_parts
+            buckets = self.parts_buckets_small if small else self.parts_buckets
+            for p in (buckets if all_parts else [top]):
                 if (b, p, 0) not in self.graphs:
                     self.capture(b, p)
 

@@ -104,11 +104,20 @@ def test_parts_buckets_cover_context():
         assert p * r.part_tokens >= kv and p in r.parts_buckets and p >= prev
         prev = p
     assert r.parts_bucket(1) == 1 and r.parts_bucket(257) == 2 and r.parts_bucket(1025) == 6
+    # small decode batches with a finer partition size bucket in their own unit
+    cfg = EngineConfig(model="tiny", device="cpu", max_model_len=3000, num_kv_blocks=64,
+                       decode_partition_tokens_small=128, decode_small_batch_max=2)
+    r = LLMEngine(cfg).runner
+    assert r.max_parts_small == 24 and r.parts_buckets_small[-1] == 24
+    assert r.parts_bucket(1025, 1) == 12 and r.parts_bucket(1025, 2) == 12
+    assert r.parts_bucket(1025, 4) == 6
+    for kv in range(1, 3001, 7):
+        assert r.parts_bucket(kv, 1) * 128 >= kv and r.parts_bucket(kv, 3) * 256 >= kv
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("buckets", [None, ()])
-def test_graph_parts_buckets_equal_eager(buckets):
+@pytest.mark.parametrize("buckets,small", [(None, 0), ((), 0), (None, 128)])
+def test_graph_parts_buckets_equal_eager(buckets, small):
     """Contexts crossing partition boundaries mid-generation (256 / 512 / 1024 tokens) replay
     graphs of several partition buckets - token-for-token equal to eager decode."""
     rng = np.random.default_rng(5)
@@ -119,6 +128,7 @@ def test_graph_parts_buckets_equal_eager(buckets):
                            max_num_seqs=8, use_graphs=graphs, graph_batch_sizes=(1, 2, 4, 8))
         if buckets is not None:
             cfg.graph_parts_buckets = buckets
+        cfg.decode_partition_tokens_small = small  # 128: batches <= 2 split finer
         eng = LLMEngine(cfg)
         # staggered finishes: the longest context leaves first, so the step's bucket walks
         # 4 -> 6 (1024 crossed) -> 4 -> 2 -> 1
