@@ -22,23 +22,34 @@ typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
-// fp8 (OCP e4m3fn on gfx950) -> 8 x 16-bit MFMA operand V (bf16x8 / f16x8).
-// v_cvt_pk_f32_fp8 turns two fp8 bytes into two floats; the pack to 16 bits is one
-// v_cvt_pk per pair.
+// fp8 (OCP e4m3fn on gfx950) -> 8 x 16-bit MFMA operand V (bf16x8 / f16x8): one
+// v_cvt_scalef32_pk_{bf16,f16}_fp8 per byte pair (scale 1.0; exact - every e4m3 value is
+// representable in bf16 and in f16), half the VALU of the f32 round trip
+// (v_cvt_pk_f32_fp8 + v_cvt_pk_bf16_f32) the fp8 decode GEMVs used to spend per pair.
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_t;
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+template <typename T>
+__device__ __forceinline__ uint32_t fp8x2_cvt(uint32_t w, bool hi);
+template <>
+__device__ __forceinline__ uint32_t fp8x2_cvt<__bf16>(uint32_t w, bool hi) {
+  return hi ? __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(
+                                               static_cast<int>(w), 1.0f, true))
+            : __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(
+                                               static_cast<int>(w), 1.0f, false));
+}
+template <>
+__device__ __forceinline__ uint32_t fp8x2_cvt<_Float16>(uint32_t w, bool hi) {
+  return hi ? __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(
+                                               static_cast<int>(w), 1.0f, true))
+            : __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(
+                                               static_cast<int>(w), 1.0f, false));
+}
 template <typename T, typename V>
 __device__ __forceinline__ V fp8x8_cvt(uint32_t lo, uint32_t hi) {
-  V f;
-  const uint32_t w[2] = {lo, hi};
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const auto a = __builtin_amdgcn_cvt_pk_f32_fp8(static_cast<int>(w[h]), false);
-    const auto b = __builtin_amdgcn_cvt_pk_f32_fp8(static_cast<int>(w[h]), true);
-    f[4 * h + 0] = static_cast<T>(a[0]);
-    f[4 * h + 1] = static_cast<T>(a[1]);
-    f[4 * h + 2] = static_cast<T>(b[0]);
-    f[4 * h + 3] = static_cast<T>(b[1]);
-  }
-  return f;
+  const u32x4 r = {fp8x2_cvt<T>(lo, false), fp8x2_cvt<T>(lo, true), fp8x2_cvt<T>(hi, false),
+                   fp8x2_cvt<T>(hi, true)};
+  return __builtin_bit_cast(V, r);
 }
 
 // 16-byte packet of eight 16-bit values.
