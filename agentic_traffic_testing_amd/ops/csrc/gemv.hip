@@ -64,22 +64,10 @@ static void launch_t(int dtype, dim3 grid, hipStream_t st, const SkinnyParams& p
   skinny_kernel<T_, WAVES, U_, MT, EPI, NT_, PS_, W8_><<<grid, blk, 0, st>>>(p)
   if (p.wscale != nullptr) {
     // fp8 weights (pre-shuffled by construction): a 16-byte lane load carries two K steps,
-    // so the stage is twice as deep to keep the same bytes in flight per wave - and twice
-    // that again when the wave's K slice is a whole number of such stages: an fp8 tile is
-    // half the bytes of a 16-bit one, so at the 2x depth a wave's whole slice (K 4096 over
-    // 8 waves: 8 KiB) is in flight in its first two stages, one memory round trip per
-    // workgroup instead of three
+    // so the stage is twice as deep to keep the same bytes in flight per wave.  (Twice that
+    // again - a wave's whole K slice in flight in its first two stages - measured slower in
+    // situ: fp8 bench 986 vs 1022 tok/s, profiles/r2_ab_fp8_stage_depth.txt.)
     constexpr int U8 = UNROLL * 2;
-    constexpr int U8D = UNROLL * 4;
-    const int kw = p.K / p.ksplit / WAVES;
-    if (kw % (32 * U8D) == 0) {
-      if (dtype == 0) {
-        if (nt) ATTA_SK(__bf16, U8D, true, true, true); else ATTA_SK(__bf16, U8D, false, true, true);
-      } else {
-        if (nt) ATTA_SK(_Float16, U8D, true, true, true); else ATTA_SK(_Float16, U8D, false, true, true);
-      }
-      return;
-    }
     if (dtype == 0) {
       if (nt) ATTA_SK(__bf16, U8, true, true, true); else ATTA_SK(__bf16, U8, false, true, true);
     } else {
