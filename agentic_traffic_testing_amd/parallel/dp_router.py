@@ -185,12 +185,15 @@ def create_app(router: Router, probe_interval_s: float = 2.0) -> web.Application
     return app
 
 
-def spawn_replicas(n: int, base_port: int, serve_args: list[str], log_dir: str = "logs"):
-    """Start n serve_llm processes, replica i pinned to GPU i."""
+def spawn_replicas(n: int, base_port: int, serve_args: list[str], log_dir: str = "logs",
+                   gpus: list[int] | None = None):
+    """Start n serve_llm processes, replica i pinned to GPU ``gpus[i]`` (default: GPU i;
+    several replicas may share a GPU, e.g. the single-GPU rehearsal test)."""
     os.makedirs(log_dir, exist_ok=True)
+    gpus = list(range(n)) if gpus is None else gpus
     procs = []
     for i in range(n):
-        env = dict(os.environ, HIP_VISIBLE_DEVICES=str(i), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        env = dict(os.environ, HIP_VISIBLE_DEVICES=str(gpus[i]), HSA_ENABLE_IPC_MODE_LEGACY="0")
         log = open(os.path.join(log_dir, f"llm_replica_{i}.log"), "a")
         procs.append(subprocess.Popen(
             [sys.executable, "-m", "agentic_traffic_testing_amd.serving.serve_llm",

@@ -81,3 +81,62 @@ def test_router_task_affinity_and_failover(backends):
         assert sorted(counts) == [0, 0, 3]  # all three on one live replica
     finally:
         rt.stop()
+
+
+@pytest.mark.gpu
+def test_router_two_gpu_replicas_one_gpu(tmp_path):
+    """Two serve_llm replica PROCESSES (the spawn_replicas path of a multi-GPU node, both
+    pinned to GPU 0 here) behind the router: concurrent /chat requests are answered by real
+    HIP engines and spread over both replicas; /health and the contract metrics work."""
+    import socket
+    import time
+
+    from agentic_traffic_testing_amd.parallel.dp_router import spawn_replicas
+
+    with socket.socket() as s0:
+        s0.bind(("127.0.0.1", 0))
+        base = s0.getsockname()[1]
+    args = ["--model", "small", "--max-model-len", "512", "--gpu-memory-utilization", "0.2",
+            "--max-num-seqs", "4"]
+    procs = spawn_replicas(2, base, args, log_dir=str(tmp_path), gpus=[0, 0])
+    rt = None
+    try:
+        urls = [f"http://127.0.0.1:{base + i}" for i in range(2)]
+        t0 = time.time()
+        for u in urls:
+            while True:
+                assert all(p.poll() is None for p in procs), open(
+                    tmp_path / "llm_replica_0.log").read()[-2000:]
+                try:
+                    if httpx.get(u + "/health", timeout=2).status_code == 200:
+                        break
+                except httpx.HTTPError:
+                    pass
+                assert time.time() - t0 < 240, "replicas did not come up"
+                time.sleep(1)
+        rt = RouterThread(Router(urls, "round_robin"))
+        import concurrent.futures as cf
+
+        def call(i):
+            r = httpx.post(rt.url + "/chat", json={"prompt": f"hello {i}", "max_tokens": 8},
+                           timeout=120)
+            r.raise_for_status()
+            return r.json()
+
+        with cf.ThreadPoolExecutor(6) as ex:
+            outs = list(ex.map(call, range(6)))
+        assert all(o["meta"]["completion_tokens"] > 0 for o in outs)
+        assert all(rep.requests >= 2 for rep in rt.router.replicas)
+        assert httpx.get(rt.url + "/health", timeout=5).status_code == 200
+        m = httpx.get(rt.url + "/metrics", timeout=5).text
+        assert "llm_requests_total" in m
+    finally:
+        if rt is not None:
+            rt.stop()
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(30)
+            except Exception:
+                p.kill()
