@@ -281,12 +281,16 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
     const int np = min(nparts, 64);
     float m_run = kNegInf, wsum = 0.f;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // partitions per round trip per thread: 8 when there are few merge groups (4-wave
+    // workgroups: NG = 4 covers 32 partitions - a 4k context at 128-token partitions - in
+    // one round trip), else 4
+    constexpr int PPI = NG <= 4 ? 8 : 4;
     if (gidx < NG) {
-      for (int u0 = 0; gidx + NG * u0 < np; u0 += 4) {
-        float lse[4];
-        f32x4 pa[4], pb[4];
+      for (int u0 = 0; gidx + NG * u0 < np; u0 += PPI) {
+        float lse[PPI];
+        f32x4 pa[PPI], pb[PPI];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < PPI; ++u) {
           const int q = min(gidx + NG * (u0 + u), np - 1);
           const int64_t base = (sh * p.max_parts + q) * 16 + mc;
           const uint32_t off = static_cast<uint32_t>((base * kD + md0) * 4);
@@ -295,7 +299,7 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
           pb[u] = __builtin_bit_cast(f32x4, dev_load16(rpo, off + 16));
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < PPI; ++u) {
           if (gidx + NG * (u0 + u) >= np || lse[u] == kNegInf) continue;  // weight 0
           const float m_new = fmaxf(m_run, lse[u]);
           const float sc = exp2f(m_run - m_new);  // m_run == -inf -> 0

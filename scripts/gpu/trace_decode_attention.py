@@ -19,6 +19,7 @@ from agentic_traffic_testing_amd import ops  # noqa: E402
 from agentic_traffic_testing_amd.ops import reference as ref  # noqa: E402
 
 HQ, HKV, H, BS, MAXP = 32, 8, 4096, 16, 32
+PT = int(os.environ.get("PT", "256"))  # partition tokens (128 / 256 / 512)
 
 
 def timeit(fn, iters=50):
@@ -42,7 +43,7 @@ def run(ctxs, dt=torch.bfloat16):
     kvlens = [c + 1 if c > 0 else 0 for c in ctxs]
     nblk = [max(1, math.ceil(kv / BS)) for kv in kvlens]
     perm = torch.randperm(sum(nblk) + 8)
-    bt = torch.zeros(B, MAXP * 256 // BS, dtype=torch.int32)
+    bt = torch.zeros(B, MAXP * 512 // BS, dtype=torch.int32)
     o = 0
     for i, n in enumerate(nblk):
         bt[i, :n] = perm[o:o + n].to(torch.int32)
@@ -75,10 +76,10 @@ def run(ctxs, dt=torch.bfloat16):
                             preshuffled=True)
 
     def attn_only():
-        ops.attention_decode_v2(q, k, v, bt, kvlen, qstart, scale, po, pl, cnt, MAXP, 256,
+        ops.attention_decode_v2(q, k, v, bt, kvlen, qstart, scale, po, pl, cnt, MAXP, PT,
                                 out=a, num_seqs=B)
 
-    print(f"== B={B} ctx={ctxs}")
+    print(f"== B={B} ctx={ctxs} partition tokens {PT}")
     print(f"  qkv {timeit(qkv_only):6.2f} us, attention {timeit(attn_only):6.2f} us", flush=True)
     qkv_only()
     atr = torch.zeros(4 * B * HKV * MAXP, dtype=torch.int64, device="cuda")
@@ -89,7 +90,7 @@ def run(ctxs, dt=torch.bfloat16):
     ops.set_attention_trace(None)
     t = atr.view(MAXP, HKV, B, 4).cpu()  # grid (seqs, heads, parts): x fastest
     real = [(s_, h, p_) for s_ in range(B) for h in range(HKV)
-            for p_ in range(math.ceil(kvlens[s_] / 256))]
+            for p_ in range(math.ceil(kvlens[s_] / PT))]
     t0 = min(int(t[p_, h, s_, 0]) for s_, h, p_ in real)
     for j, name in enumerate(("past RT1", "computed", "published", "end")):
         c = sorted((int(t[p_, h, s_, j]) - t0) / 100.0 for s_, h, p_ in real)
