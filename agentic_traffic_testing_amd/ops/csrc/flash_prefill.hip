@@ -5,7 +5,7 @@
 // GQA G = Hq / Hkv in {1, 2, 3, 4, 8}, head_dim 128, bf16 / fp16 (G = 3: Llama-3.2-3B, 24 q /
 // 8 kv heads; a wave's last 32 mod 3 = 2 columns idle).
 //
-// Work decomposition: grid (tiles, Hkv).  A workgroup = 4 waves owns 128 "columns" = the G
+// Work decomposition: grid tiles x Hkv (1-D, KV head fastest).  A workgroup = 4 waves owns 128 "columns" = the G
 // query heads of one KV head x 128 / G consecutive query tokens of one sequence; wave w owns
 // columns 32w..32w+31 (column c: token c / G, head c % G).  Every K/V tile is staged ONCE in
 // LDS per workgroup and read by all 128 columns (G x the reuse of a per-head kernel).
@@ -96,9 +96,14 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
   const int wid = tid >> 6;
   const int r = lane & 31;   // column within the wave / row within a 32-row operand
   const int h = lane >> 5;   // lane half
-  // heaviest (latest-token) tiles first: tiles are emitted in token order per sequence
-  const int tile = p.num_tiles - 1 - static_cast<int>(blockIdx.x);
-  const int hk = blockIdx.y;
+  // 1-D grid, KV head fastest: blocks are dealt round-robin over the 8 XCDs, so with 8 KV
+  // heads every tile of head hk runs on one XCD and the head's K/V (re-read by all its
+  // tiles) stays in that XCD's L2 instead of being pulled into all eight (placement is a
+  // speed choice only, never correctness).  Heaviest (latest-token) tiles first: tiles are
+  // emitted in token order per sequence.
+  const int bid = static_cast<int>(blockIdx.x);
+  const int hk = bid % p.n_kv_heads;
+  const int tile = p.num_tiles - 1 - bid / p.n_kv_heads;
   const int s = p.tile_seq[tile];
   const int qoff = p.tile_qoff[tile];
   const int kvlen = p.seq_kvlen[s];  // >= wg_end: every key this workgroup reads is below it
@@ -354,7 +359,7 @@ int atta_flash_prefill(void* out, const void* q, const void* k_cache, const void
   prm.n_kv_heads = n_kv_heads;
   prm.bs_shift = shift;
   prm.scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid(num_tiles, n_kv_heads);
+  dim3 grid(num_tiles * n_kv_heads);
   const int rc = dtype == 0 ? fp::launch<__bf16>(G, grid, stream, prm)
                             : fp::launch<_Float16>(G, grid, stream, prm);
   if (rc) return rc;
