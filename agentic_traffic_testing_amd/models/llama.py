@@ -392,13 +392,10 @@ class LlamaModel:
             ops.decode_qkv_rope(residual, wq, eps, md.positions, md.slot_mapping, self.cos_sin,
                                 k_caches[li], v_caches[li], nq, nkv, q_out=q, preshuffled=ps,
                                 w_scale=L.qkv_s)
-            wo = L.o_ps if ps else L.o
-            pf = (ops.oproj_prefetch_spec(wo, wo.shape[0], ops.decode_waves("o", ps, L.o_s is not None),
-                                          B, nkv, ws["pf_sink"]) if ps and "pf_sink" in ws else None)
             ops.attention_decode_v2(q, k_caches[li], v_caches[li], md.block_tables,
                                     md.seq_kvlen, md.seq_qstart, self.scale, ws["part_out"],
                                     ws["part_lse"], ws["counters"], ws["max_parts"],
-                                    ws["part_tokens"], out=attn, num_seqs=B, prefetch=pf)
+                                    ws["part_tokens"], out=attn, num_seqs=B)
             a2 = attn.view(B, nq * self.head_dim)
             if self.tp_size == 1:
                 ops.linear(a2, L.o_ps if ps else L.o, residual=residual,

@@ -556,42 +556,16 @@ def set_attention_trace(trace=None):
     _native().set_attention_trace(trace)
 
 
-# L2 prefetch of the o_proj weights by extra workgroups of the decode attention launch
-# (attention_decode.hip prefetch_body): 4 KiB chunks per o_proj wave slice (0 = off) and the
-# prefetch workgroups per XCD.  A/B in profiles/r2_ab_oproj_prefetch.txt.
-OPROJ_PREFETCH_CHUNKS = int(os.environ.get("ATTA_OPROJ_PREFETCH", "0"))
-OPROJ_PREFETCH_WGS = int(os.environ.get("ATTA_OPROJ_PREFETCH_WGS", "8"))
-
-
-def oproj_prefetch_spec(w: torch.Tensor, n_out: int, waves: int, num_seqs: int,
-                        n_kv_heads: int, sink: torch.Tensor, chunks: int | None = None):
-    """Prefetch argument tuple for ``attention_decode_v2`` covering the pre-shuffled o_proj
-    weight ``w`` ([n_out, K], 16-row tiles, ``waves`` K slices per tile), or None."""
-    chunks = OPROJ_PREFETCH_CHUNKS if chunks is None else chunks
-    if chunks <= 0 or not w.is_cuda or n_out % 16:
-        return None
-    tiles = n_out // 16
-    slice_bytes = w.numel() * w.element_size() // tiles // waves
-    chunks = min(chunks, slice_bytes // 4096)
-    if chunks <= 0:
-        return None
-    wg_per_z = num_seqs * n_kv_heads
-    z = max(1, -(-OPROJ_PREFETCH_WGS * 8 // wg_per_z))
-    return (w, tiles, waves, chunks, z, sink)
-
-
 def attention_decode_v2(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, scale,
                         part_out, part_lse, counters, max_parts, part_tokens, out=None,
-                        num_seqs: int = -1, prefetch=None):
-    """Decode attention with in-kernel split-K combine (one launch).  ``prefetch``
-    (``oproj_prefetch_spec``) adds workgroups that warm the next GEMV's weights in L2."""
+                        num_seqs: int = -1):
+    """Decode attention with in-kernel split-K combine (one launch)."""
     if not q.is_cuda:
         n = seq_kvlen.shape[0] if num_seqs < 0 else num_seqs
         return ref.paged_attention(q, k_cache, v_cache, block_tables[:n], seq_kvlen[:n],
                                    seq_qstart[:n + 1], scale, out=out)
     out = torch.empty_like(q) if out is None else out
-    pf = prefetch or (None, 0, 0, 0, 0, None)
     _native().attention_decode_v2(out, part_out, part_lse, counters, q, k_cache, v_cache,
                                   block_tables, seq_kvlen, seq_qstart, num_seqs, max_parts,
-                                  part_tokens, q.shape[1], k_cache.shape[1], scale, *pf)
+                                  part_tokens, q.shape[1], k_cache.shape[1], scale)
     return out

@@ -66,60 +66,7 @@ struct DecParams {
   float scale_log2;
   // optional per-workgroup timeline (100 MHz wall clock): [start, past-wait, end, hw id]
   unsigned long long* wg_trace;
-  // L2 prefetch of the NEXT GEMV's weights (o_proj) by pf_z extra grid z-slices (see
-  // prefetch_body); pf_base == nullptr: off
-  const uint8_t* pf_base;
-  int64_t pf_tile_bytes;  // bytes of one 16-row tile (pre-shuffled: contiguous)
-  int pf_tiles, pf_slice_bytes, pf_chunks, pf_z;
-  unsigned* pf_sink;
 };
-
-// Decode attention is latency bound (~2-3 dependent round trips per workgroup, a few MB of
-// KV) while HBM idles; the o_proj GEMV that follows streams 32-34 MB cold.  Extra
-// workgroups of this launch load the first pf_chunks x 4 KiB of every wave slice of every
-// o_proj tile into the L2 of the XCD that will run that tile: the GEMV's 1-D grid puts tile
-// t on XCD t % 8 (round-robin dispatch), and this launch's workgroup with linear id l runs on
-// XCD l % 8, so prefetch workgroup l covers tiles t == l (mod 8).  Plain (allocating) dword
-// loads, one per 64 B per lane (4 KiB per wave instruction), 8 in flight per wave; the
-// values are folded and stored only under a runtime-false test, so nothing is written.
-template <int WAVES>
-__device__ __forceinline__ void prefetch_body(const DecParams& p) {
-  const int lane = threadIdx.x & 63;
-  // wave-uniform loop bounds (scalar): no divergent control flow in front of the attention
-  // body's scalar-operand asm
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t gxy = static_cast<int64_t>(gridDim.x) * gridDim.y;
-  const int64_t lin = blockIdx.x + gridDim.x * (blockIdx.y + static_cast<int64_t>(gridDim.y) * blockIdx.z);
-  const int64_t base = gxy * p.max_parts;
-  const int64_t total = gxy * (p.max_parts + p.pf_z);
-  const int xcd = static_cast<int>(lin & 7);
-  const int64_t first = base + ((xcd - base) & 7);  // first prefetch workgroup on this XCD
-  const int idx = static_cast<int>((lin - first) >> 3);
-  const int cnt = static_cast<int>((total - first + 7) >> 3);
-  const int tiles_x = (p.pf_tiles - xcd + 7) >> 3;  // tiles xcd, xcd + 8, ...
-  const int slices = static_cast<int>(p.pf_tile_bytes / p.pf_slice_bytes);
-  const int per_tile = slices * p.pf_chunks;
-  const int items = tiles_x * per_tile;
-  const int stride = cnt * WAVES;
-  unsigned acc = 0u;
-  for (int i0 = idx * WAVES + wid; i0 < items; i0 += 8 * stride) {
-    unsigned v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = min(i0 + u * stride, items - 1);
-      const int t = xcd + 8 * (i / per_tile);
-      const int r = i % per_tile;
-      const int64_t off = t * p.pf_tile_bytes + static_cast<int64_t>(r / p.pf_chunks) * p.pf_slice_bytes +
-                          (r % p.pf_chunks) * 4096 + lane * 64;
-      v[u] = *reinterpret_cast<const unsigned*>(p.pf_base + off);
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) acc ^= v[u];
-  }
-  // never taken (pf_tiles > 0, checked on the host) but opaque to the compiler, which
-  // would otherwise drop the loads (a provably dead store - e.g. a lane test - does that)
-  if (acc == 0x9e3779b9u && p.pf_tiles < 0) p.pf_sink[0] = acc;
-}
 
 template <typename T>
 struct TileFrags {
@@ -127,7 +74,7 @@ struct TileFrags {
   i16x4 v[8];
 };
 
-template <typename T, int G, int WAVES, int TPW, bool PF = false>
+template <typename T, int G, int WAVES, int TPW>
 __device__ __forceinline__ void decode_attention_body(const DecParams& p, const int s,
                                                       const int hk, const int part,
                                                       unsigned long long (&tr)[3]) {
@@ -156,14 +103,10 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
   }
   int kvlen = p.seq_kvlen[s];
   int qrow = p.seq_qstart[s + 1] - 1;
-  // one wait for all of them (keeps the compiler from chaining the loads behind branches).
-  // Not in the prefetch variant (PF): with the prefetch branch in the kernel the compiler
-  // cannot keep these in SGPRs (illegal VGPR -> SGPR copy)
-  if constexpr (!PF) {
-    asm volatile("" : "+s"(kvlen), "+s"(qrow));
+  // one wait for all of them (keeps the compiler from chaining the loads behind branches)
+  asm volatile("" : "+s"(kvlen), "+s"(qrow));
 #pragma unroll
-    for (int i = 0; i < TPW; ++i) asm volatile("" : "+s"(bte[i]));
-  }
+  for (int i = 0; i < TPW; ++i) asm volatile("" : "+s"(bte[i]));
   // timeline probe: clock reads only after the scalar loads above - an earlier one makes
   // them vector loads, which the scalar-operand asm cannot take
   tr[0] = wall_clock64();
@@ -400,16 +343,10 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
     __hip_atomic_store(p.counters + sh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <typename T, int G, int WAVES, int TPW, bool PF>
+template <typename T, int G, int WAVES, int TPW>
 __global__ __launch_bounds__(WAVES * 64) void decode_attention_kernel(DecParams p) {
-  if constexpr (PF) {
-    if (blockIdx.z >= p.max_parts) {  // block-uniform: L2 prefetch workgroup
-      prefetch_body<WAVES>(p);
-      return;
-    }
-  }
   unsigned long long tr[3] = {0, 0, 0};
-  decode_attention_body<T, G, WAVES, TPW, PF>(p, blockIdx.x, blockIdx.y, blockIdx.z, tr);
+  decode_attention_body<T, G, WAVES, TPW>(p, blockIdx.x, blockIdx.y, blockIdx.z, tr);
   // timeline probe (set_attention_trace): [past round trip 1, computed, published, end]
   if (p.wg_trace != nullptr && threadIdx.x == 0) {
     const int64_t b = blockIdx.x + static_cast<int64_t>(gridDim.x) *
@@ -421,14 +358,14 @@ __global__ __launch_bounds__(WAVES * 64) void decode_attention_kernel(DecParams 
   }
 }
 
-template <typename T, int WAVES, int TPW, bool PF>
+template <typename T, int WAVES, int TPW>
 static int launch_g(int G, dim3 grid, hipStream_t st, const DecParams& p) {
   switch (G) {
-    case 1: decode_attention_kernel<T, 1, WAVES, TPW, PF><<<grid, WAVES * 64, 0, st>>>(p); return 0;
-    case 2: decode_attention_kernel<T, 2, WAVES, TPW, PF><<<grid, WAVES * 64, 0, st>>>(p); return 0;
-    case 3: decode_attention_kernel<T, 3, WAVES, TPW, PF><<<grid, WAVES * 64, 0, st>>>(p); return 0;
-    case 4: decode_attention_kernel<T, 4, WAVES, TPW, PF><<<grid, WAVES * 64, 0, st>>>(p); return 0;
-    case 8: decode_attention_kernel<T, 8, WAVES, TPW, PF><<<grid, WAVES * 64, 0, st>>>(p); return 0;
+    case 1: decode_attention_kernel<T, 1, WAVES, TPW><<<grid, WAVES * 64, 0, st>>>(p); return 0;
+    case 2: decode_attention_kernel<T, 2, WAVES, TPW><<<grid, WAVES * 64, 0, st>>>(p); return 0;
+    case 3: decode_attention_kernel<T, 3, WAVES, TPW><<<grid, WAVES * 64, 0, st>>>(p); return 0;
+    case 4: decode_attention_kernel<T, 4, WAVES, TPW><<<grid, WAVES * 64, 0, st>>>(p); return 0;
+    case 8: decode_attention_kernel<T, 8, WAVES, TPW><<<grid, WAVES * 64, 0, st>>>(p); return 0;
     default: return -1;
   }
 }
@@ -437,11 +374,10 @@ static int launch_g(int G, dim3 grid, hipStream_t st, const DecParams& p) {
 // 512 = 16 x 2 (16 waves cap VGPRs at 128: more tiles per wave would spill).
 template <typename T>
 static int launch(int G, int part_tokens, dim3 grid, hipStream_t st, const DecParams& p) {
-  const bool pf = p.pf_z > 0;
   switch (part_tokens) {
-    case 128: return pf ? launch_g<T, 4, 2, true>(G, grid, st, p) : launch_g<T, 4, 2, false>(G, grid, st, p);
-    case 256: return pf ? launch_g<T, 8, 2, true>(G, grid, st, p) : launch_g<T, 8, 2, false>(G, grid, st, p);
-    case 512: return pf ? launch_g<T, 16, 2, true>(G, grid, st, p) : launch_g<T, 16, 2, false>(G, grid, st, p);
+    case 128: return launch_g<T, 4, 2>(G, grid, st, p);
+    case 256: return launch_g<T, 8, 2>(G, grid, st, p);
+    case 512: return launch_g<T, 16, 2>(G, grid, st, p);
     default: return -1;
   }
 }
@@ -464,8 +400,6 @@ int atta_attention_decode_v2(void* out, float* part_out, float* part_lse, int* c
                              int num_seqs, int max_parts, int part_tokens, int n_q_heads,
                              int n_kv_heads, int head_dim, int block_size, int bt_stride,
                              int64_t q_stride, int64_t out_stride, float scale, int dtype,
-                             const void* pf_base, int64_t pf_tile_bytes, int pf_tiles,
-                             int pf_slice_bytes, int pf_chunks, int pf_z, unsigned* pf_sink,
                              hipStream_t stream) {
   const int G = n_q_heads / n_kv_heads;
   int shift = 0;
@@ -494,19 +428,7 @@ int atta_attention_decode_v2(void* out, float* part_out, float* part_lse, int* c
   p.max_parts = max_parts;
   p.scale_log2 = scale * 1.4426950408889634f;
   p.wg_trace = g_attn_trace;
-  if (pf_base != nullptr && pf_z > 0 && pf_chunks > 0) {
-    if (pf_slice_bytes < pf_chunks * 4096 || pf_tile_bytes % pf_slice_bytes != 0 ||
-        pf_tiles < 1 || pf_sink == nullptr)
-      return -1;
-    p.pf_base = static_cast<const uint8_t*>(pf_base);
-    p.pf_tile_bytes = pf_tile_bytes;
-    p.pf_tiles = pf_tiles;
-    p.pf_slice_bytes = pf_slice_bytes;
-    p.pf_chunks = pf_chunks;
-    p.pf_z = pf_z;
-    p.pf_sink = pf_sink;
-  }
-  dim3 grid(num_seqs, n_kv_heads, max_parts + p.pf_z);
+  dim3 grid(num_seqs, n_kv_heads, max_parts);
   const int rc = dtype == 0 ? dec::launch<__bf16>(G, part_tokens, grid, stream, p)
                             : dec::launch<_Float16>(G, part_tokens, grid, stream, p);
   if (rc) return rc;

@@ -440,10 +440,7 @@ void attention_decode_v2(at::Tensor out, at::Tensor part_out, at::Tensor part_ls
                          const at::Tensor& v_cache, const at::Tensor& block_tables,
                          const at::Tensor& seq_kvlen, const at::Tensor& seq_qstart,
                          int64_t num_seqs, int64_t max_parts, int64_t part_tokens,
-                         int64_t n_q_heads, int64_t n_kv_heads, double scale,
-                         const c10::optional<at::Tensor>& pf_weight, int64_t pf_tiles,
-                         int64_t pf_slices, int64_t pf_chunks, int64_t pf_z,
-                         const c10::optional<at::Tensor>& pf_sink) {
+                         int64_t n_q_heads, int64_t n_kv_heads, double scale) {
   check_dev(q, "q");
   TORCH_CHECK(block_tables.scalar_type() == at::kInt && seq_kvlen.scalar_type() == at::kInt &&
                   seq_qstart.scalar_type() == at::kInt && counters.scalar_type() == at::kInt,
@@ -454,23 +451,6 @@ void attention_decode_v2(at::Tensor out, at::Tensor part_out, at::Tensor part_ls
                   part_lse.numel() >= num_seqs * n_kv_heads * max_parts * 16 &&
                   counters.numel() >= num_seqs * n_kv_heads,
               "attention_decode_v2: workspace too small");
-  const void* pf_base = nullptr;
-  int64_t pf_tile_bytes = 0, pf_slice_bytes = 0;
-  unsigned* sink = nullptr;
-  if (pf_weight.has_value() && pf_z > 0 && pf_chunks > 0) {
-    // o_proj weights, pre-shuffled (16-row tiles of contiguous bytes) - any dtype
-    TORCH_CHECK(pf_sink.has_value() && pf_sink->is_cuda() && pf_weight->is_cuda() &&
-                    pf_weight->is_contiguous() && pf_tiles > 0 && pf_slices > 0,
-                "attention_decode_v2: prefetch arguments");
-    const int64_t nbytes = pf_weight->numel() * pf_weight->element_size();
-    TORCH_CHECK(nbytes % pf_tiles == 0 && (nbytes / pf_tiles) % pf_slices == 0,
-                "attention_decode_v2: prefetch tiling");
-    pf_tile_bytes = nbytes / pf_tiles;
-    pf_slice_bytes = pf_tile_bytes / pf_slices;
-    TORCH_CHECK(pf_chunks * 4096 <= pf_slice_bytes, "attention_decode_v2: prefetch chunks");
-    pf_base = pf_weight->data_ptr();
-    sink = reinterpret_cast<unsigned*>(pf_sink->data_ptr());
-  }
   const at::DeviceGuard g(q.device());
   check_rc(atta_attention_decode_v2(
                out.data_ptr(), part_out.data_ptr<float>(), part_lse.data_ptr<float>(),
@@ -478,9 +458,7 @@ void attention_decode_v2(at::Tensor out, at::Tensor part_out, at::Tensor part_ls
                block_tables.data_ptr<int>(), seq_kvlen.data_ptr<int>(), seq_qstart.data_ptr<int>(),
                num_seqs, max_parts, part_tokens, n_q_heads, n_kv_heads, k_cache.size(3),
                k_cache.size(2), block_tables.stride(0), q.stride(0), out.stride(0),
-               static_cast<float>(scale), dtype_code(q), pf_base, pf_tile_bytes,
-               static_cast<int>(pf_tiles), static_cast<int>(pf_slice_bytes),
-               static_cast<int>(pf_chunks), static_cast<int>(pf_z), sink, cur_stream()),
+               static_cast<float>(scale), dtype_code(q), cur_stream()),
            "attention_decode_v2");
 }
 
@@ -607,8 +585,7 @@ TORCH_LIBRARY(atta, m) {
       "attention_decode_v2(Tensor(a!) out, Tensor(b!) part_out, Tensor(c!) part_lse, "
       "Tensor(d!) counters, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
       "Tensor seq_kvlen, Tensor seq_qstart, int num_seqs, int max_parts, int part_tokens, "
-      "int n_q_heads, int n_kv_heads, float scale, Tensor? pf_weight=None, int pf_tiles=0, "
-      "int pf_slices=0, int pf_chunks=0, int pf_z=0, Tensor? pf_sink=None) -> ()");
+      "int n_q_heads, int n_kv_heads, float scale) -> ()");
   m.def(
       "fused_qkv_rope(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor x, "
       "Tensor w, Tensor positions, Tensor slots, Tensor cos_sin, int n_q_heads, int n_kv_heads, "

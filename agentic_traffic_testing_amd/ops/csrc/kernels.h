@@ -92,8 +92,6 @@ int atta_attention_decode_v2(void* out, float* part_out, float* part_lse, int* c
                              int num_seqs, int max_parts, int part_tokens, int n_q_heads,
                              int n_kv_heads, int head_dim, int block_size, int bt_stride,
                              int64_t q_stride, int64_t out_stride, float scale, int dtype,
-                             const void* pf_base, int64_t pf_tile_bytes, int pf_tiles,
-                             int pf_slice_bytes, int pf_chunks, int pf_z, unsigned* pf_sink,
                              hipStream_t stream);
 
 int atta_skinny_variant(void* y, const void* x, const void* w, int M, int N, int K,

@@ -523,41 +523,6 @@ def test_attention_decode_v2_grid_invariant():
         assert torch.equal(o, outs[0])
 
 
-@pytest.mark.parametrize("n_seqs,pf_wgs", [(1, 8), (3, 5), (4, 16)])
-@pytest.mark.parametrize("fp8", [False, True])
-def test_attention_decode_v2_oproj_prefetch(n_seqs, pf_wgs, fp8, monkeypatch):
-    """The o_proj L2-prefetch workgroups appended to the decode attention grid change no
-    output bit, write nothing (the sink stays zero) and keep their loads inside the weight
-    (odd sequence counts: prefetch workgroups that do not start on XCD 0)."""
-    torch.manual_seed(13)
-    dt, bs, hq, hkv = torch.bfloat16, 16, 32, 8
-    seqs = [(300 + 517 * i, 1) for i in range(n_seqs)]
-    k, v, bt, kvlen, qstart, T = _make_paged(seqs, hkv, bs, dt)
-    q = torch.randn(T, hq, 128, dtype=dt, device="cuda")
-    S, scale, max_parts = n_seqs, 1 / math.sqrt(128), 32
-    po = torch.empty(S * hkv * max_parts * 16 * 128, device="cuda")
-    pl = torch.empty(S * hkv * max_parts * 16, device="cuda")
-    cnt = torch.zeros(S * hkv, dtype=torch.int32, device="cuda")
-    H = hq * 128
-    w = torch.randn(H, H, dtype=dt, device="cuda") * 0.02
-    wo = (ops.preshuffle_fp8(ops.quantize_fp8(w)[0]) if fp8 else ops.preshuffle(w))
-    sink = torch.zeros(4, dtype=torch.int32, device="cuda")
-    monkeypatch.setattr(ops, "OPROJ_PREFETCH_WGS", pf_wgs)
-    outs = []
-    for chunks in (0, 1, 2, 64):
-        pf = ops.oproj_prefetch_spec(wo, H, ops.decode_waves("o", True, fp8), S, hkv, sink,
-                                     chunks=chunks)
-        assert (pf is None) == (chunks == 0)
-        out = torch.full_like(q, 3.0)
-        ops.attention_decode_v2(q, k, v, bt, kvlen, qstart, scale, po, pl, cnt, max_parts, 128,
-                                out=out, prefetch=pf)
-        torch.cuda.synchronize()
-        outs.append(out)
-        assert bool((cnt == 0).all()) and bool((sink == 0).all())
-    for o in outs[1:]:
-        assert torch.equal(o, outs[0])
-
-
 @pytest.mark.parametrize("m", [1, 5, 20])
 def test_preshuffled_decode_kernels_bit_identical(m, monkeypatch):
     """Pre-shuffled weights feed the same lanes the same products in the same order, so every
