@@ -25,7 +25,8 @@ def close(a, b, atol, rtol=0.0):
 
 
 @pytest.mark.parametrize("dtype", DT)
-@pytest.mark.parametrize("shape", [(1, 4096), (7, 4096), (33, 8192), (300, 1024), (5, 3072)])
+@pytest.mark.parametrize("shape", [(1, 4096), (7, 4096), (33, 8192), (300, 1024), (5, 3072),
+                                   (2600, 4096), (3, 16384)])
 def test_rms_norm(dtype, shape):
     torch.manual_seed(0)
     x = torch.randn(shape, dtype=dtype, device="cuda")
@@ -34,7 +35,7 @@ def test_rms_norm(dtype, shape):
 
 
 @pytest.mark.parametrize("dtype", DT)
-@pytest.mark.parametrize("shape", [(1, 4096), (9, 4096), (128, 8192)])
+@pytest.mark.parametrize("shape", [(1, 4096), (9, 4096), (128, 8192), (5, 16384)])
 def test_fused_add_rms_norm(dtype, shape):
     torch.manual_seed(1)
     x = torch.randn(shape, dtype=dtype, device="cuda")
@@ -78,13 +79,16 @@ def _rand_cache(nb, hkv, bs, d, dtype):
 
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (8, 1), (4, 1), (24, 8)])
-def test_rope_cache(dtype, hq, hkv):
+@pytest.mark.parametrize("T", [5, 37, 300])  # < 16: per-token kernel; else 16-token tiles
+def test_rope_cache(dtype, hq, hkv, T):
     torch.manual_seed(3)
-    T, D, bs, nb = 37, 128, 16, 64
+    D, bs, nb = 128, 16, 64
     qkv = torch.randn(T, (hq + 2 * hkv) * D, dtype=dtype, device="cuda")
     pos = torch.randint(0, 4000, (T,), dtype=torch.int32, device="cuda")
     slots = torch.randperm(nb * bs, device="cuda")[:T].to(torch.int32)
-    slots[5] = -1
+    if T == 300:  # pages filled in order from mid-page (the prefill case the tiles coalesce)
+        slots = torch.arange(T, dtype=torch.int32, device="cuda") + 40
+    slots[T // 2] = -1
     cs = ref.rope_cos_sin(D, 8192, 500000.0, {"rope_type": "llama3", "factor": 8.0,
                                               "low_freq_factor": 1.0, "high_freq_factor": 4.0,
                                               "original_max_position_embeddings": 8192},
