@@ -65,6 +65,18 @@ void silu_and_mul(at::Tensor out, const at::Tensor& x) {
 
 // prev (int64) is read only while *feed_prev != 0, i.e. for async-decode look-ahead steps
 // (decode batches, rows <= the sampler output buffer); prefill steps leave the flag 0.
+void stream_read(const at::Tensor& x, at::Tensor sink) {
+  TORCH_CHECK(x.is_cuda() && sink.is_cuda() && x.is_contiguous() && sink.scalar_type() == at::kInt,
+              "stream_read: CUDA tensors, int32 sink");
+  const int64_t bytes = x.numel() * x.element_size();
+  TORCH_CHECK(bytes % 16 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "stream_read: 16-byte aligned, whole 16-byte words");
+  const at::DeviceGuard g(x.device());
+  check_rc(atta_stream_read(x.data_ptr(), bytes, reinterpret_cast<unsigned*>(sink.data_ptr()),
+                            static_cast<int>(sink.numel()), cur_stream()),
+           "stream_read");
+}
+
 void embed(at::Tensor out, const at::Tensor& table, const at::Tensor& ids,
            const c10::optional<at::Tensor>& prev, const c10::optional<at::Tensor>& feed_prev) {
   check_dev(table, "table");
@@ -606,6 +618,7 @@ TORCH_LIBRARY(atta, m) {
   m.def("fused_add_rms_norm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
   m.def("embed(Tensor(a!) out, Tensor table, Tensor ids, Tensor? prev, Tensor? feed_prev) -> ()");
+  m.def("stream_read(Tensor x, Tensor(a!) sink) -> ()");
   m.def(
       "rope_cache(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor qkv, "
       "Tensor positions, Tensor slot_mapping, Tensor cos_sin, int n_q_heads, int n_kv_heads, "
@@ -635,6 +648,7 @@ TORCH_LIBRARY_IMPL(atta, CUDA, m) {
   m.impl("fused_add_rms_norm", &fused_add_rms_norm);
   m.impl("silu_and_mul", &silu_and_mul);
   m.impl("embed", &embed);
+  m.impl("stream_read", &stream_read);
   m.impl("rope_cache", &rope_cache);
   m.impl("attention_prefill", &attention_prefill);
   m.impl("flash_prefill", &flash_prefill);

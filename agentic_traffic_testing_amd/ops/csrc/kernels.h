@@ -16,6 +16,8 @@ int atta_rms_norm(void* out, void* residual, const void* x, const void* w, int r
 
 int atta_silu_and_mul(void* out, const void* x, int rows, int inter, int64_t x_stride,
                       int64_t out_stride, int dtype, hipStream_t stream);
+int atta_stream_read(const void* x, int64_t bytes, unsigned* sink, int blocks,
+                     hipStream_t stream);
 int atta_embed(void* out, const void* table, const int* ids, const int64_t* prev,
                const int* feed_prev, int rows, int hidden, int64_t vocab, int64_t out_stride,
                hipStream_t stream);

@@ -5,7 +5,8 @@ import torch
 from agentic_traffic_testing_amd.ops import build
 
 EXPECTED_OPS = {
-    "rms_norm", "fused_add_rms_norm", "silu_and_mul", "embed", "rope_cache", "attention_prefill",
+    "rms_norm", "fused_add_rms_norm", "silu_and_mul", "embed", "stream_read", "rope_cache",
+    "attention_prefill",
     "attention_decode", "attention_decode_v2", "sample", "skinny_gemm", "fused_qkv_rope",
     "fused_gate_up_silu", "fused_lm_head_sample", "sample_finalize", "skinny_variant",
     "ar_buffer_bytes", "ar_alloc", "ar_free", "ar_handle", "ar_open", "ar_close", "ar_error",
