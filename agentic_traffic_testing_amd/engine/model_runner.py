@@ -193,7 +193,6 @@ class ModelRunner:
             "tokens": torch.zeros(self.max_seqs, dtype=torch.int64, device=dev),
             "tp_keys": torch.zeros(self.max_seqs, dtype=torch.int64, device=dev),
             "counters": torch.zeros(self.max_seqs * nkv, dtype=torch.int32, device=dev),
-            "pf_sink": torch.zeros(4, dtype=torch.int32, device=dev),
             "part_out": self.part_out, "part_lse": self.part_lse,
             "max_parts": self.max_parts, "part_tokens": self.part_tokens,
         }

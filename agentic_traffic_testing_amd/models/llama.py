@@ -384,19 +384,11 @@ class LlamaModel:
         q = ws["q"][:B]
         attn = ws["attn"][:B]
         act = ws["act"][:B]
-        nl = len(self.layers)
-        pf = ops.GEMV_PREFETCH_CHUNKS > 0 and "pf_sink" in ws
-
-        def arm(w, proj, scale):  # next GEMV's weights, prefetched in this launch's tail
-            if pf and w is not None:
-                ops.set_gemv_prefetch(w, proj, scale is not None, ws["pf_sink"])
-
         for li, L in enumerate(self.layers):
             ps = L.qkv_ps is not None
             if L.qkv_s is not None and not ps:
                 raise RuntimeError("fp8 decode needs prepare_decode_weights()")
             wq = L.qkv_ps if ps else L.qkv
-            arm(L.o_ps, "o", L.o_s)
             ops.decode_qkv_rope(residual, wq, eps, md.positions, md.slot_mapping, self.cos_sin,
                                 k_caches[li], v_caches[li], nq, nkv, q_out=q, preshuffled=ps,
                                 w_scale=L.qkv_s)
@@ -405,7 +397,6 @@ class LlamaModel:
                                     ws["part_lse"], ws["counters"], ws["max_parts"],
                                     ws["part_tokens"], out=attn, num_seqs=B)
             a2 = attn.view(B, nq * self.head_dim)
-            arm(L.gate_up_ps, "gate_up", L.gate_up_s)
             if self.tp_size == 1:
                 ops.linear(a2, L.o_ps if ps else L.o, residual=residual,
                            waves=ops.decode_waves("o", ps, L.o_s is not None),
@@ -414,12 +405,8 @@ class LlamaModel:
                 residual.add_(self._all_reduce(ops.linear(a2, L.o_ps if ps else L.o,
                                                           preshuffled=ps, w_scale=L.o_s,
                                                           ksplit=None, proj="o")))
-            arm(L.down_ps, "down", L.down_s)
             ops.decode_gate_up_silu(residual, L.gate_up_ps if ps else L.gate_up, eps, out=act,
                                     preshuffled=ps, w_scale=L.gate_up_s)
-            if li + 1 < nl:
-                nxt = self.layers[li + 1]
-                arm(nxt.qkv_ps, "qkv", nxt.qkv_s)
             if self.tp_size == 1:
                 ops.linear(act, L.down_ps if ps else L.down, residual=residual,
                            waves=ops.decode_waves("down", ps, L.down_s is not None),

@@ -549,25 +549,6 @@ def key_to_token(keys: torch.Tensor) -> torch.Tensor:
     return 0xFFFFFFFF - (keys & 0xFFFFFFFF)
 
 
-# Tail prefetch of the next decode GEMV's weights (skinny.h gemv_tail_prefetch): 4 KiB chunks
-# per wave slice of the next kernel's first GEMV_PREFETCH_TILES tiles (0 = off).  A/B in
-# profiles/r2_ab_gemv_tail_prefetch.txt.
-GEMV_PREFETCH_CHUNKS = int(os.environ.get("ATTA_GEMV_PREFETCH", "0"))
-GEMV_PREFETCH_TILES = int(os.environ.get("ATTA_GEMV_PREFETCH_TILES", "512"))
-
-
-def set_gemv_prefetch(w, proj: str, fp8: bool, sink, chunks: int | None = None):
-    """Arm the NEXT skinny GEMV launch on this thread to prefetch, in its tail, the first
-    chunks of the pre-shuffled weight ``w`` that the decode GEMV ``proj`` after it streams
-    (``w`` None or chunks 0: disarm).  Hint only: outputs do not change."""
-    chunks = GEMV_PREFETCH_CHUNKS if chunks is None else chunks
-    if w is None or chunks <= 0 or not w.is_cuda:
-        _native().set_gemv_prefetch(None, 0, 0, 0, None)
-        return
-    tiles = min(w.shape[0] // 16, GEMV_PREFETCH_TILES)
-    _native().set_gemv_prefetch(w, tiles, decode_waves(proj, True, fp8), chunks, sink)
-
-
 def set_attention_trace(trace=None):
     """Per-workgroup timeline of the decode attention launches that follow (int64 CUDA tensor
     of 4 words per workgroup of the (seqs, kv heads, partitions) grid: past round trip 1,

@@ -474,26 +474,6 @@ void attention_decode_v2(at::Tensor out, at::Tensor part_out, at::Tensor part_ls
            "attention_decode_v2");
 }
 
-void set_gemv_prefetch(const c10::optional<at::Tensor>& w, int64_t tiles, int64_t slices,
-                       int64_t chunks, const c10::optional<at::Tensor>& sink) {
-  if (!w.has_value() || tiles <= 0 || chunks <= 0) {
-    check_rc(atta_set_gemv_prefetch(nullptr, 0, 0, 0, 0, 0, nullptr), "set_gemv_prefetch");
-    return;
-  }
-  TORCH_CHECK(w->is_cuda() && w->is_contiguous() && sink.has_value() && sink->is_cuda() &&
-                  w->size(0) % 16 == 0 && slices > 0,
-              "set_gemv_prefetch: contiguous CUDA weight with 16-row tiles, CUDA sink");
-  const int64_t tile_bytes = w->numel() * w->element_size() / (w->size(0) / 16);
-  TORCH_CHECK(tile_bytes % slices == 0 && tiles <= w->size(0) / 16,
-              "set_gemv_prefetch: tiling");
-  const int64_t slice_bytes = tile_bytes / slices;
-  check_rc(atta_set_gemv_prefetch(w->data_ptr(), tile_bytes, static_cast<int>(tiles),
-                                  static_cast<int>(slice_bytes), static_cast<int>(slices),
-                                  static_cast<int>(std::min<int64_t>(chunks, slice_bytes / 4096)),
-                                  reinterpret_cast<unsigned*>(sink->data_ptr())),
-           "set_gemv_prefetch");
-}
-
 void set_attention_trace(const c10::optional<at::Tensor>& trace) {
   if (trace.has_value()) {
     TORCH_CHECK(trace->scalar_type() == at::kLong && trace->is_contiguous() && trace->is_cuda(),
@@ -603,8 +583,6 @@ TORCH_LIBRARY(atta, m) {
   m.def("ar_buffer_bytes(int max_elems, int elem_bytes) -> int", &ar_buffer_bytes);
   m.def("ar_alloc(int bytes, int device) -> int", &ar_alloc);
   m.def("set_attention_trace(Tensor? trace) -> ()", &set_attention_trace);
-  m.def("set_gemv_prefetch(Tensor? w, int tiles, int slices, int chunks, Tensor? sink) -> ()",
-        &set_gemv_prefetch);
   m.def("ar_free(int ptr) -> ()", &ar_free);
   m.def("ar_handle(int ptr) -> Tensor", &ar_handle);
   m.def("ar_open(Tensor handle) -> int", &ar_open);

@@ -37,9 +37,7 @@ template <typename T, int WAVES, int UNROLL, int MT, int EPI, bool NTL = false, 
           bool W8 = false>
 __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
   skinny_body<T, WAVES, UNROLL, MT, EPI, NTL, PS, W8>(p, blockIdx.x, blockIdx.y);
-  if (p.nx_w != nullptr) gemv_tail_prefetch<WAVES>(p);  // grid-uniform
 }
-
 
 // Weight-stream cache policy.  Non-temporal (nt) weight loads: every decode weight byte is
 // read once per step by one CU, so keeping it out of the caches helps - but only with the
@@ -172,41 +170,6 @@ __global__ void __launch_bounds__(kFinThreads) sample_finalize_kernel(
 
 using namespace atta;
 
-// Next-weight tail prefetch for the following skinny launch (ops.set_gemv_prefetch): armed by
-// the host, consumed (and cleared) by the next launch on this thread.
-static SkinnyParams g_next{};
-static bool g_next_armed = false;
-
-int atta_set_gemv_prefetch(const void* w, int64_t tile_bytes, int tiles, int slice_bytes,
-                           int slices, int chunks, unsigned* sink) {
-  g_next_armed = false;
-  if (w == nullptr || tiles <= 0 || chunks <= 0) return 0;
-  if (slices <= 0 || slice_bytes < chunks * 4096 ||
-      static_cast<int64_t>(slice_bytes) * slices != tile_bytes || sink == nullptr)
-    return -1;
-  g_next.nx_w = static_cast<const uint8_t*>(w);
-  g_next.nx_tile_bytes = tile_bytes;
-  g_next.nx_tiles = tiles;
-  g_next.nx_slice_bytes = slice_bytes;
-  g_next.nx_slices = slices;
-  g_next.nx_chunks = chunks;
-  g_next.nx_sink = sink;
-  g_next_armed = true;
-  return 0;
-}
-
-static void take_prefetch(SkinnyParams& p) {
-  if (!g_next_armed) return;
-  p.nx_w = g_next.nx_w;
-  p.nx_tile_bytes = g_next.nx_tile_bytes;
-  p.nx_tiles = g_next.nx_tiles;
-  p.nx_slice_bytes = g_next.nx_slice_bytes;
-  p.nx_slices = g_next.nx_slices;
-  p.nx_chunks = g_next.nx_chunks;
-  p.nx_sink = g_next.nx_sink;
-  g_next_armed = false;
-}
-
 static int skinny_checks(int M, int K, int waves) {
   if (M < 1 || M > 32) return -1;
   if (K % (32 * waves) != 0) return -1;
@@ -269,7 +232,6 @@ int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual
   p.x_stride = x_stride;
   p.eps = 0.f;
   if (const int rc = setup_split(p, waves, ksplit, N / 16, wscale != nullptr)) return rc;
-  if (p.ksplit == 1) take_prefetch(p);
   const int mt = M <= 16 ? 1 : 2;
   dim3 grid(N / 16, p.ksplit);
   if (residual != nullptr) {
@@ -319,7 +281,6 @@ int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x
   p.n_kv_heads = n_kv_heads;
   p.bs_shift = shift;
   if (const int rc = setup_split(p, waves, ksplit, p.N / 16, wscale != nullptr)) return rc;
-  if (p.ksplit == 1) take_prefetch(p);
   dim3 grid(p.N / 16, p.ksplit);
   launch_epi<EPI_QKVROPE>(dtype, M <= 16 ? 1 : 2, waves, grid, stream, p);
   return static_cast<int>(hipGetLastError());
@@ -345,7 +306,6 @@ int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int 
   p.inter = inter;
   p.eps = eps;
   if (const int rc = setup_split(p, waves, ksplit, inter / 8, wscale != nullptr)) return rc;
-  if (p.ksplit == 1) take_prefetch(p);
   dim3 grid(inter / 8, p.ksplit);
   launch_epi<EPI_SILU>(dtype, M <= 16 ? 1 : 2, waves, grid, stream, p);
   return static_cast<int>(hipGetLastError());

@@ -91,47 +91,7 @@ struct SkinnyParams {
   int ksplit;
   float* sk_ws;
   int* sk_counters;
-  // tail prefetch of the NEXT decode GEMV's weights (gemv_tail_prefetch); nx_w == nullptr: off
-  const uint8_t* nx_w;
-  int64_t nx_tile_bytes;  // bytes per 16-row tile of the next weight (pre-shuffled, contiguous)
-  int nx_tiles, nx_slice_bytes, nx_slices, nx_chunks;
-  unsigned* nx_sink;
 };
-
-// Tail prefetch (decode weight chain): after its own tile, each of this launch's LAST
-// workgroups loads the first nx_chunks x 4 KiB of every wave slice of next-kernel tiles
-// t' == its own index (mod grid size), t' < nx_tiles (the host passes the next kernel's
-// first dispatch rounds).  Both grids are 1-D and multiples of 8, so t' lands on the XCD
-// that will run it (round-robin dispatch) and the next kernel's first loads hit its L2
-// instead of paying the HBM ramp.  The loads overlap this kernel's drain, when HBM is no
-// longer saturated.  Values are folded and stored only under a runtime-false test.
-template <int WAVES>
-__device__ __forceinline__ void gemv_tail_prefetch(const SkinnyParams& p) {
-  const int T = gridDim.x;
-  const int b = blockIdx.x;
-  const int first = T > p.nx_tiles ? T - p.nx_tiles : 0;  // only the last workgroups
-  if (b < first) return;
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int per_tile = p.nx_slices * p.nx_chunks;
-  unsigned acc = 0u;
-  for (int t = b - first; t < p.nx_tiles; t += T) {
-    const uint8_t* base = p.nx_w + t * p.nx_tile_bytes;
-    for (int i0 = wid; i0 < per_tile; i0 += 4 * WAVES) {
-      unsigned v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = min(i0 + u * WAVES, per_tile - 1);
-        v[u] = *reinterpret_cast<const unsigned*>(
-            base + static_cast<int64_t>(i / p.nx_chunks) * p.nx_slice_bytes +
-            (i % p.nx_chunks) * 4096 + lane * 64);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc ^= v[u];
-    }
-  }
-  if (acc == 0x9e3779b9u && p.nx_tiles < 0) p.nx_sink[0] = acc;  // nx_tiles > 0: never
-}
 
 __device__ __forceinline__ unsigned ordered_bits(float f) {
   const unsigned u = __float_as_uint(f);

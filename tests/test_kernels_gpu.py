@@ -527,34 +527,6 @@ def test_attention_decode_v2_grid_invariant():
         assert torch.equal(o, outs[0])
 
 
-@pytest.mark.parametrize("fp8", [False, True])
-def test_gemv_tail_prefetch_changes_nothing(fp8):
-    """A skinny launch armed with the next GEMV's weight prefetch returns the same bits, leaves
-    the sink untouched, and the arming is consumed by exactly one launch (next weight larger
-    and smaller than the grid; chunks past the slice clamp)."""
-    torch.manual_seed(14)
-    dt, K = torch.bfloat16, 4096
-    x = torch.randn(3, K, dtype=dt, device="cuda")
-    w = torch.randn(4096, K, dtype=dt, device="cuda") * 0.02
-    prep = ((lambda a, m="plain": ops.preshuffle_fp8(ops.quantize_fp8(a)[0], m)) if fp8
-            else (lambda a, m="plain": ops.preshuffle(a, m)))
-    wp = prep(w)
-    ws = ops.quantize_fp8(w)[1] if fp8 else None
-    nxt_big = prep(torch.randn(28672, K, dtype=dt, device="cuda"), "silu")
-    nxt_small = prep(torch.randn(1024, K, dtype=dt, device="cuda"))
-    sink = torch.zeros(4, dtype=torch.int32, device="cuda")
-    waves = ops.decode_waves("o", True, fp8)
-    ref_out = ops.linear(x, wp, waves=waves, preshuffled=True, w_scale=ws, ksplit=None)
-    for nxt, proj, chunks in ((nxt_big, "gate_up", 1), (nxt_small, "o", 64), (nxt_big, "down", 3)):
-        ops.set_gemv_prefetch(nxt, proj, fp8, sink, chunks=chunks)
-        got = ops.linear(x, wp, waves=waves, preshuffled=True, w_scale=ws, ksplit=None)
-        again = ops.linear(x, wp, waves=waves, preshuffled=True, w_scale=ws, ksplit=None)
-        torch.cuda.synchronize()
-        assert torch.equal(got, ref_out) and torch.equal(again, ref_out)
-        assert bool((sink == 0).all())
-    ops.set_gemv_prefetch(None, "o", fp8, sink)
-
-
 @pytest.mark.parametrize("m", [1, 5, 20])
 def test_preshuffled_decode_kernels_bit_identical(m, monkeypatch):
     """Pre-shuffled weights feed the same lanes the same products in the same order, so every
