@@ -194,11 +194,12 @@ def spawn_replicas(n: int, base_port: int, serve_args: list[str], log_dir: str =
     procs = []
     for i in range(n):
         env = dict(os.environ, HIP_VISIBLE_DEVICES=str(gpus[i]), HSA_ENABLE_IPC_MODE_LEGACY="0")
-        log = open(os.path.join(log_dir, f"llm_replica_{i}.log"), "a")
-        procs.append(subprocess.Popen(
-            [sys.executable, "-m", "agentic_traffic_testing_amd.serving.serve_llm",
-             "--host", "127.0.0.1", "--port", str(base_port + i), *serve_args],
-            env=env, stdout=log, stderr=subprocess.STDOUT))
+        # the child inherits its own copy of the log descriptor; the parent's closes here
+        with open(os.path.join(log_dir, f"llm_replica_{i}.log"), "a") as log:
+            procs.append(subprocess.Popen(
+                [sys.executable, "-m", "agentic_traffic_testing_amd.serving.serve_llm",
+                 "--host", "127.0.0.1", "--port", str(base_port + i), *serve_args],
+                env=env, stdout=log, stderr=subprocess.STDOUT))
     return procs
 
 
