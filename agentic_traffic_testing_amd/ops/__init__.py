@@ -36,6 +36,13 @@ def library_build_hash(path: Path = _LIB) -> str | None:
     return fn().decode()
 
 
+def _lib_embeds(digest: str) -> bool:
+    try:
+        return digest.encode() in _LIB.read_bytes()
+    except OSError:
+        return False
+
+
 def load_native(build_if_missing: bool = True) -> bool:
     """Load the HIP kernel library.  With ``build_if_missing`` the library is (re)built
     in-tree when missing or when its sources changed (content-hash stamps); without it a
@@ -46,9 +53,12 @@ def load_native(build_if_missing: bool = True) -> bool:
     try:
         from . import build
 
-        if build_if_missing:
-            build.build_kernels()  # no-op when every stamp matches
         want = build.kernel_source_hash()
+        # a library that embeds the current source hash is used as is (checked on the file
+        # bytes, without loading it): the object files and their stamps need not exist - a
+        # gpurun snapshot ships the .so only, and N ranks importing at once must not rebuild
+        if build_if_missing and not _lib_embeds(want):
+            build.build_kernels()  # serialised across processes by a file lock
         got = library_build_hash()
         if got != want:
             raise RuntimeError(f"stale kernel library {_LIB}: built from sources {got}, "

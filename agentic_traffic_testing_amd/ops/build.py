@@ -24,6 +24,8 @@ from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
+import contextlib
+import fcntl
 import hashlib
 import os
 import shutil
@@ -100,8 +102,25 @@ def _run(cmd):
     return r
 
 
-def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> Path:
+@contextlib.contextmanager
+def _build_lock():
+    """Exclusive inter-process lock around a build: ranks that import the package at the
+    same time build once, in turn, instead of writing the same objects concurrently."""
     BUILD.mkdir(parents=True, exist_ok=True)
+    with open(BUILD / ".build.lock", "w") as f:
+        fcntl.flock(f, fcntl.LOCK_EX)
+        try:
+            yield
+        finally:
+            fcntl.flock(f, fcntl.LOCK_UN)
+
+
+def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> Path:
+    with _build_lock():
+        return _build_kernels(force, jobs, verbose)
+
+
+def _build_kernels(force: bool, jobs: int, verbose: bool) -> Path:
     headers = sorted(CSRC.glob("*.h"))
     hdr_digest = _files_digest(headers)
     src_hash = kernel_source_hash()
@@ -173,6 +192,11 @@ def runtime_flags(extra=()) -> list[str]:
 
 
 def build_runtime(force: bool = False) -> Path:
+    with _build_lock():
+        return _build_runtime(force)
+
+
+def _build_runtime(force: bool) -> Path:
     target = runtime_so_path()
     srcs = sorted(RUNTIME_CSRC.glob("*.cpp"))
     if not srcs:

@@ -67,3 +67,36 @@ def test_runtime_embeds_source_hash():
     from agentic_traffic_testing_amd import runtime
 
     assert runtime.BUILD_HASH == build.runtime_source_hash()
+
+
+def test_current_library_is_used_without_object_files(tmp_path, monkeypatch):
+    """A gpurun snapshot ships the .so but not _build/*.o: a library that embeds the current
+    source hash must load as is (no rebuild - N DP ranks import at once), and a stale one is
+    detected from its bytes."""
+    from agentic_traffic_testing_amd import ops
+
+    build.build_kernels()
+    assert ops._lib_embeds(build.kernel_source_hash())
+    assert not ops._lib_embeds("0" * 32)
+    calls = []
+    monkeypatch.setattr(build, "build_kernels", lambda *a, **k: calls.append(1))
+    monkeypatch.setattr(ops, "_loaded", False)
+    assert ops.load_native(build_if_missing=True), ops._load_error
+    assert calls == []
+
+
+def test_build_lock_serialises_processes(tmp_path):
+    """Two processes holding the build lock never overlap."""
+    import subprocess
+    import sys
+
+    log = tmp_path / "log"
+    code = (
+        "import time, sys\n"
+        "from agentic_traffic_testing_amd.ops import build\n"
+        "with build._build_lock():\n"
+        f"    open({str(log)!r}, 'a').write('in\\n'); time.sleep(0.5)\n"
+        f"    open({str(log)!r}, 'a').write('out\\n')\n")
+    ps = [subprocess.Popen([sys.executable, "-c", code]) for _ in range(2)]
+    assert all(p.wait(timeout=60) == 0 for p in ps)
+    assert log.read_text().split() == ["in", "out", "in", "out"]

@@ -678,3 +678,14 @@ def test_gemm_fp8_rowwise(m):
         (wq.view(torch.float8_e4m3fn).float() * ws[:, None]).t()
     err = (got.float() - exp).abs().max() / exp.abs().max()
     assert float(err) < 1e-2
+
+
+@pytest.mark.parametrize("nbytes", [16, 4096 + 48, 64 << 20])
+def test_stream_read_probe(nbytes):
+    """The HBM read probe (scripts/gpu/decode_sol.py) reads whole buffers of any 16-byte
+    multiple, including a grid-stride remainder, and writes nothing."""
+    x = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device="cuda")
+    sink = torch.zeros(512, dtype=torch.int32, device="cuda")
+    ops._native().stream_read(x, sink)
+    torch.cuda.synchronize()
+    assert bool((sink == 0).all())
