@@ -639,7 +639,8 @@ def test_fp8_prefill_linear():
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2, 3])
-@pytest.mark.parametrize("m,width", [(1, 4096), (37, 8192), (300, 14336)])
+@pytest.mark.parametrize("m,width", [(1, 4096), (37, 8192), (300, 14336), (3, 28672),
+                                     (2, 40960)])  # 40960: past the register-resident sizes
 def test_quant_rows_fp8(mode, m, width):
     """Fused row-wise e4m3fn quantisation (norm / silu-mul / plain) vs the fp32 reference:
     scales match, codes dequantise to the reference values within e4m3 rounding."""
