@@ -361,11 +361,12 @@ class ModelRunner:
                                     prev_tokens=self.ws["tokens"], feed_prev=v["feed_prev"],
                                     top_p=v["top_p"] if special else None, top_k=v["top_k"])
         decode_only = md.num_tiles == 0 and md.num_decode == T
-        hidden = m.forward(v["input_ids"], md, self.k_layers, self.v_layers, self.part_out,
-                           self.part_lse, num_parts, self.part_tokens,
-                           prev_tokens=self.ws["tokens"] if decode_only else None,
-                           feed_prev=v["feed_prev"] if decode_only else None)
-        last = hidden.index_select(0, v["logits_idx"])
+        # final norm on the sampled rows only (each sequence's last token)
+        last = m.forward(v["input_ids"], md, self.k_layers, self.v_layers, self.part_out,
+                         self.part_lse, num_parts, self.part_tokens,
+                         prev_tokens=self.ws["tokens"] if decode_only else None,
+                         feed_prev=v["feed_prev"] if decode_only else None,
+                         rows=v["logits_idx"])
         if not special and m.decode_fusable(last.shape[0]) and \
                 last.shape[0] <= self.max_seqs and m.hidden_fusable():
             # fused LM head + Gumbel-max sampler on the (already normalised) last rows

@@ -295,8 +295,10 @@ class LlamaModel:
 
     def forward(self, input_ids: torch.Tensor, md: AttnMeta, k_caches, v_caches,
                 part_out=None, part_lse=None, num_parts: int = 1, part_tokens: int = 256,
-                prev_tokens=None, feed_prev=None):
-        """Returns the final normed hidden state rows [T, H]."""
+                prev_tokens=None, feed_prev=None, rows: torch.Tensor | None = None):
+        """Returns the final normed hidden state rows [T, H] - or only ``rows`` (int64 row
+        indices, e.g. each sequence's last token) when given: the final norm then runs on
+        those rows alone."""
         cfg = self.cfg
         eps = cfg.rms_norm_eps
         # the residual stream IS the embedding output: every row-parallel projection adds its
@@ -344,6 +346,9 @@ class LlamaModel:
             gu = self._proj(x, L.gate_up, L.gate_up_s)
             a = ops.silu_and_mul(gu)
             self._proj_residual(a, L.down, L.down_s, residual)
+        if rows is not None:
+            residual = residual.index_select(0, rows)
+            pending = None if pending is None else pending.index_select(0, rows)
         if pending is not None:
             return ops.fused_add_rms_norm(pending, residual, self.norm, eps)
         return ops.rms_norm(residual, self.norm, eps)
