@@ -149,9 +149,58 @@ def embed(table: torch.Tensor, ids: torch.Tensor, prev: torch.Tensor | None = No
     return out
 
 
+# Bounds-checked debug mode: ATTA_DEBUG_CHECKS=1 validates every paged-KV
+# launch's block-table / slot / length arguments against the cache before the kernel runs
+# (the kernels themselves index unchecked: a bad page id there is an out-of-bounds HBM access
+# that can fault the GPU).  Checks synchronise with the device, so they are skipped inside
+# hipGraph capture; combine with HIP_LAUNCH_BLOCKING=1 to pin a fault to its launch.
+DEBUG_CHECKS = os.environ.get("ATTA_DEBUG_CHECKS", "0") == "1"
+
+
+class PagedArgsError(ValueError):
+    pass
+
+
+def _capturing(t: torch.Tensor) -> bool:
+    return t.is_cuda and torch.cuda.is_current_stream_capturing()
+
+
+def check_paged_args(k_cache, block_tables, seq_kvlen, num_seqs: int = -1, what: str = ""):
+    """Every block-table entry a sequence's kvlen reaches names a cache page, and the table
+    row is long enough.  Raises PagedArgsError (debug mode only; no-op while capturing)."""
+    if not DEBUG_CHECKS or _capturing(block_tables):
+        return
+    n = seq_kvlen.shape[0] if num_seqs < 0 else num_seqs
+    nb, bs = k_cache.shape[0], k_cache.shape[2]
+    bt = block_tables[:n].long()
+    kv = seq_kvlen[:n].long()
+    need = (kv + bs - 1) // bs
+    if n and int(need.max()) > bt.shape[1]:
+        raise PagedArgsError(f"{what}: kvlen {int(kv.max())} needs {int(need.max())} pages, "
+                             f"block table has {bt.shape[1]} columns")
+    used = torch.arange(bt.shape[1], device=bt.device)[None, :] < need[:, None]
+    bad = used & ((bt < 0) | (bt >= nb))
+    if bool(bad.any()):
+        s, c = (int(i) for i in bad.nonzero()[0])
+        raise PagedArgsError(f"{what}: sequence {s} page slot {c} = {int(bt[s, c])} outside "
+                             f"the cache's {nb} pages")
+
+
+def check_slots(k_cache, slots, what: str = ""):
+    """KV-write slots are -1 (skip) or inside the cache.  Debug mode only."""
+    if not DEBUG_CHECKS or _capturing(slots) or slots.numel() == 0:
+        return
+    cap = k_cache.shape[0] * k_cache.shape[2]
+    sl = slots.long()
+    if bool(((sl < -1) | (sl >= cap)).any()):
+        raise PagedArgsError(f"{what}: slot ids outside [-1, {cap}): "
+                             f"min {int(sl.min())}, max {int(sl.max())}")
+
+
 def rope_cache(qkv, positions, slot_mapping, cos_sin, k_cache, v_cache, n_q_heads, n_kv_heads,
                head_dim, q_out: torch.Tensor | None = None):
     """Rotate q/k, write k/v to the paged cache; returns q [T, Hq, D]."""
+    check_slots(k_cache, slot_mapping, "rope_cache")
     if not qkv.is_cuda:
         q = ref.rope_cache(qkv, positions, slot_mapping, cos_sin, k_cache, v_cache, n_q_heads,
                            n_kv_heads, head_dim)
@@ -185,6 +234,7 @@ def attention_prefill(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, 
                       tile_qoff, scale, out=None, impl: str | None = None):
     """Causal varlen prefill attention over the paged cache.  ``tile_seq`` / ``tile_qoff``
     must come from tiles of ``prefill_tile_tokens(G, impl)`` tokens."""
+    check_paged_args(k_cache, block_tables, seq_kvlen, what="attention_prefill")
     if not q.is_cuda:
         return ref.paged_attention(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart,
                                    scale, out=out)
@@ -199,6 +249,7 @@ def attention_prefill(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, 
 def attention_decode(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, scale,
                      part_out, part_lse, num_parts, part_tokens, out=None, num_seqs: int = -1):
     """Decode attention for sequences [0, num_seqs) (one query token each)."""
+    check_paged_args(k_cache, block_tables, seq_kvlen, num_seqs, "attention_decode")
     if not q.is_cuda:
         n = seq_kvlen.shape[0] if num_seqs < 0 else num_seqs
         return ref.paged_attention(q, k_cache, v_cache, block_tables[:n], seq_kvlen[:n],
@@ -495,6 +546,7 @@ def decode_qkv_rope(x, w, eps, positions, slots, cos_sin, k_cache, v_cache, n_q_
                     n_kv_heads, q_out=None, preshuffled=False, w_scale=None, ksplit=None):
     """RMSNorm(x) -> QKV GEMM -> RoPE -> q out + paged K/V write, one kernel on the GPU."""
     _need_cuda(x, preshuffled or w_scale is not None)
+    check_slots(k_cache, slots[:x.shape[0]], "decode_qkv_rope")
     if q_out is None:
         q_out = torch.empty(x.shape[0], n_q_heads, 128, dtype=x.dtype, device=x.device)
     if not x.is_cuda:
@@ -570,6 +622,7 @@ def attention_decode_v2(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart
                         part_out, part_lse, counters, max_parts, part_tokens, out=None,
                         num_seqs: int = -1):
     """Decode attention with in-kernel split-K combine (one launch)."""
+    check_paged_args(k_cache, block_tables, seq_kvlen, num_seqs, "attention_decode_v2")
     if not q.is_cuda:
         n = seq_kvlen.shape[0] if num_seqs < 0 else num_seqs
         return ref.paged_attention(q, k_cache, v_cache, block_tables[:n], seq_kvlen[:n],
