@@ -102,6 +102,14 @@ MODEL_PRESETS: dict[str, ModelConfig] = {
                                   num_kv_heads=8, tie_word_embeddings=True,
                                   rope_scaling=dict(LLAMA3_ROPE_SCALING, factor=32.0),
                                   bos_token_id=16000, eos_token_ids=(16001, 16009)),
+    # the Llama-3-70B TP=8 per-rank geometry (one KV head and 8 q heads per rank, hidden 8192)
+    # with an FFN that stays fused-decode-shaped at TP=2/4/8 (7168 / 8 = 896 = 7 x 128): the
+    # one-GPU TP rehearsal of graph-captured decode
+    "llama-70b-tp-slice": ModelConfig(name="llama-70b-tp-slice", vocab_size=16384,
+                                      hidden_size=8192, intermediate_size=7168, num_layers=2,
+                                      num_heads=64, num_kv_heads=8, rope_scaling=None,
+                                      max_position_embeddings=16384, bos_token_id=16000,
+                                      eos_token_ids=(16001, 16009)),
     "llama-70b-slice": ModelConfig(name="llama-70b-slice", vocab_size=16384, hidden_size=8192,
                                    intermediate_size=3584, num_layers=2, num_heads=64,
                                    num_kv_heads=8, rope_scaling=None,

@@ -177,7 +177,16 @@ class AsyncEngine:
                 continue
             now = time.monotonic()
             for o in outs:
-                last = self._last_sent.get(o.request_id)
+                rid = o.request_id
+                if rid not in self._streams:
+                    # the consumer already left (disconnect): its generate() popped the
+                    # entry; re-adding it here would leak one dict slot per disconnect
+                    self._last_sent.pop(rid, None)
+                    continue
+                last = self._last_sent.get(rid)
                 if o.finished or last is None or now - last >= self.stream_interval_s:
-                    self._last_sent[o.request_id] = now
-                    self._deliver(o.request_id, o)
+                    if o.finished:
+                        self._last_sent.pop(rid, None)
+                    else:
+                        self._last_sent[rid] = now
+                    self._deliver(rid, o)

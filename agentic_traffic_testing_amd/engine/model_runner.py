@@ -149,8 +149,6 @@ class ModelRunner:
             | {self.max_parts_small})
         self.tile_tokens = ops.prefill_tile_tokens(self.model.g)
         self.graph_sizes = sorted(b for b in cfg.graph_batch_sizes)
-        if comm is not None and comm.size > 1 and comm.is_gloo:
-            self.graph_sizes = []  # gloo collectives are host-side: nothing to capture
         cap = next((b for b in self.graph_sizes if b >= cfg.max_num_seqs), cfg.max_num_seqs)
         self.graph_sizes = [b for b in self.graph_sizes if b <= cap]
         self.max_seqs = max(cfg.max_num_seqs, self.graph_sizes[-1] if self.graph_sizes else 1)
@@ -216,7 +214,12 @@ class ModelRunner:
         torch.cuda.synchronize(self.device)
         free, total = torch.cuda.mem_get_info(self.device)
         keep = max(int(0.15 * total), 24 << 30)  # KV cache + activations + graphs
-        if need > free - keep:
+        ok = int(need <= free - keep)
+        if self.comm is not None and self.comm.size > 1:
+            # every TP rank must pick the same GEMV layout (ranks sharing a GPU, or loading at
+            # different times, see different free memory): the group decides by MIN
+            ok = self.comm.min_int(ok, self.device)
+        if not ok:
             print(f"[atta] skipping pre-shuffled decode weights: {need / 2**30:.1f} GiB needed, "
                   f"{free / 2**30:.1f} GiB free (row-major decode GEMVs)", flush=True)
             return False
@@ -372,19 +375,35 @@ class ModelRunner:
             # fused LM head + Gumbel-max sampler on the (already normalised) last rows
             return m.sample_rows(last, 0.0, v["temperature"], v["seeds"], v["steps"], self.ws)
         logits = m.compute_logits(last)
+        # decode-only steps sample straight into ws["tokens"]: a graph replay (and the next
+        # look-ahead step's embed) reads the samples from there, so the captured sampler must
+        # write them there too (a fresh tensor would leave the previous step's tokens behind)
+        out = self.ws["tokens"][:logits.shape[0]] if decode_only else None
         if special:
             return ops.sample_topkp(logits, v["temperature"], v["top_p"], v["top_k"],
-                                    v["seeds"], v["steps"])
-        return ops.sample(logits, v["temperature"], v["seeds"], v["steps"])
+                                    v["seeds"], v["steps"], out=out)
+        return ops.sample(logits, v["temperature"], v["seeds"], v["steps"], out=out)
 
     # ------------------------------------------------------------------------------------
+    def _graph_ok(self, bucket: int, special: bool = False) -> bool:
+        """Can a decode step of this bucket be captured?  Every collective inside it must be
+        device-side: RCCL, or - on a gloo control group (TP ranks rehearsing on one GPU) - the
+        IPC kernels, which carry the fused decode step's X1/X2 sums and X4 key MAX but not the
+        logits all-gather of the top-k / top-p sampler or of buckets past the fused path."""
+        c = self.comm
+        if c is None or c.size == 1 or not c.is_gloo:
+            return True
+        return (c.decode_capturable and not special and self.fused_decode
+                and self.model.decode_fusable(bucket))
+
     def graph_bucket(self, batch: Batch) -> int:
         """Graph bucket a decode-only batch replays from (0: eager step)."""
         n = len(batch.seqs)
         if not (self.is_cuda and self.cfg.use_graphs and batch.num_decode == n and n > 0
                 and self.graph_sizes and n <= self.graph_sizes[-1]):
             return 0
-        return next(b for b in self.graph_sizes if b >= n)
+        b = next(b for b in self.graph_sizes if b >= n)
+        return b if self._graph_ok(b, self._special(batch)) else 0
 
     @staticmethod
     def _special(batch: Batch) -> bool:
@@ -587,13 +606,24 @@ class ModelRunner:
                 self._forward_sample(v, md, parts, special)
         torch.cuda.current_stream(self.device).wait_stream(stream)
         g = torch.cuda.CUDAGraph()
+        dump_dir = os.environ.get("ATTA_GRAPH_DUMP_DIR")
+        if dump_dir:  # node-level dump of every captured step (scripts/gpu/graph_nodes.py)
+            g.enable_debug_mode()
         if self.graph_pool is None:
             self.graph_pool = torch.cuda.graph_pool_handle()
         with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
             out = self._forward_sample(v, md, parts, special)
+            toks = self.ws["tokens"]
+            if out.data_ptr() != toks.data_ptr():  # every sampler path ends in ws["tokens"]
+                toks[:bucket].copy_(out[:bucket])
+                out = toks[:bucket]
         self.ws["tokens"].copy_(saved_tokens)
         torch.cuda.synchronize(self.device)
         key = (bucket, parts, int(special))
+        if dump_dir:
+            os.makedirs(dump_dir, exist_ok=True)
+            g.debug_dump(os.path.join(
+                dump_dir, f"tp{self.tp_size}_rank{self.tp_rank}_b{bucket}_p{parts}_s{int(special)}.dot"))
         self.graphs[key] = g
         self.graph_io[key] = {"layout": lay, "dev": dev, "out": out}
 
@@ -603,6 +633,8 @@ class ModelRunner:
         if not (self.is_cuda and self.cfg.use_graphs):
             return
         for b in self.graph_sizes:
+            if not self._graph_ok(b):
+                continue
             small = self._small(b)
             top = self.max_parts_small if small else self.max_parts
             buckets = self.parts_buckets_small if small else self.parts_buckets

@@ -356,8 +356,8 @@ class LlamaModel:
     def _proj_residual(self, x, w, scale, residual):
         """residual += x @ w.T (row-parallel projection; TP: all-reduced partial sums)."""
         if self.tp_size > 1:
-            residual.add_(self._all_reduce(self._proj(x, w, scale)))
-            return residual
+            # residual += sum over ranks, the add fused into the IPC reduction's epilogue
+            return self.tp_group.all_reduce_residual(self._proj(x, w, scale), residual)
         return self._proj(x, w, scale, residual=residual)
 
     def decode_fusable(self, num_tokens: int) -> bool:
@@ -407,9 +407,9 @@ class LlamaModel:
                            waves=ops.decode_waves("o", ps, L.o_s is not None),
                            preshuffled=ps, w_scale=L.o_s, ksplit=None, proj="o")
             else:
-                residual.add_(self._all_reduce(ops.linear(a2, L.o_ps if ps else L.o,
-                                                          preshuffled=ps, w_scale=L.o_s,
-                                                          ksplit=None, proj="o")))
+                self.tp_group.all_reduce_residual(
+                    ops.linear(a2, L.o_ps if ps else L.o, preshuffled=ps, w_scale=L.o_s,
+                               ksplit=None, proj="o"), residual)
             ops.decode_gate_up_silu(residual, L.gate_up_ps if ps else L.gate_up, eps, out=act,
                                     preshuffled=ps, w_scale=L.gate_up_s)
             if self.tp_size == 1:
@@ -418,9 +418,9 @@ class LlamaModel:
                            preshuffled=ps, w_scale=L.down_s, ksplit=None,
                            proj="down")
             else:
-                residual.add_(self._all_reduce(ops.linear(act, L.down_ps if ps else L.down,
-                                                          preshuffled=ps, w_scale=L.down_s,
-                                                          ksplit=None, proj="down")))
+                self.tp_group.all_reduce_residual(
+                    ops.linear(act, L.down_ps if ps else L.down, preshuffled=ps,
+                               w_scale=L.down_s, ksplit=None, proj="down"), residual)
         if top_p is not None:
             logits = self.compute_logits(ops.rms_norm(residual, self.norm, eps))
             return ops.sample_topkp(logits, temperature, top_p, top_k, seeds, steps,
@@ -444,9 +444,8 @@ class LlamaModel:
                                          tokens=ws["tp_keys"][:B], finalize="key",
                                          vocab_offset=self.tp_rank * self.vocab_shard,
                                          preshuffled=lm_ps)
-        self.tp_group.all_reduce_max(keys)
         toks = ws["tokens"][:B]
-        toks.copy_(ops.key_to_token(keys))
+        self.tp_group.all_reduce_max(keys, tokens=toks)  # IPC: one kernel, tokens included
         return toks
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:

@@ -51,9 +51,13 @@ __device__ __forceinline__ uint16_t* slot_ptr(uint8_t* base, int par, int src,
   return reinterpret_cast<uint16_t*>(base + kHeaderBytes) + (par * kMaxRanks + src) * max_elems;
 }
 
+// res != nullptr: y = bf16(bf16(sum) + res) - the row-parallel projection's residual-stream
+// update fused into the reduction (the same two roundings as residual.add_(all_reduce(x)),
+// without the extra launch and HBM pass); y may alias res.
 template <typename T, int W>
 __global__ void __launch_bounds__(kThreads) oneshot_kernel(Params p, const uint16_t* x,
-                                                           uint16_t* y, int64_t n) {
+                                                           uint16_t* y, const uint16_t* res,
+                                                           int64_t n) {
   const int b = blockIdx.x;
   const int nb = gridDim.x;
   uint8_t* mine = p.base[p.rank];
@@ -117,6 +121,15 @@ __global__ void __launch_bounds__(kThreads) oneshot_kernel(Params p, const uint1
         for (int j = 0; j < 8; ++j) acc[j] += to_f32<T>(v.v[j]);
       } else {
         for (int j = 0; j < cnt; ++j) acc[j] += to_f32<T>(src[j]);
+      }
+    }
+    if (res != nullptr) {
+      if (cnt == 8) {
+        const V r = *reinterpret_cast<const V*>(res + i);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = to_f32<T>(from_f32<T>(acc[j])) + to_f32<T>(r.v[j]);
+      } else {
+        for (int j = 0; j < cnt; ++j) acc[j] = to_f32<T>(from_f32<T>(acc[j])) + to_f32<T>(res[i + j]);
       }
     }
     if (cnt == 8) {
@@ -194,7 +207,8 @@ __device__ __forceinline__ void raise_and_wait(uint8_t* const* bases, uint8_t* m
 
 template <typename T, int W>
 __global__ void __launch_bounds__(kThreads) twoshot_kernel(Params2 p, const uint16_t* x,
-                                                           uint16_t* y, int64_t n) {
+                                                           uint16_t* y, const uint16_t* res,
+                                                           int64_t n) {
   using V = Pack8;
   const int b = blockIdx.x;
   const int me = p.rank;
@@ -278,10 +292,15 @@ __global__ void __launch_bounds__(kThreads) twoshot_kernel(Params2 p, const uint
     span(q, lo, hi);
     const uint16_t* src = slot2_ptr<W>(mine, 1, par, q, p.chunk_max) + off - lo;
     for (int64_t i = lo + 8 * threadIdx.x; i < hi; i += 8 * kThreads) {
-      if (i + 8 <= hi)
+      if (res != nullptr) {  // residual-stream update fused (see oneshot_kernel)
+        const int cnt = i + 8 <= hi ? 8 : static_cast<int>(hi - i);
+        for (int j = 0; j < cnt; ++j)
+          y[i + j] = from_f32<T>(to_f32<T>(src[i + j]) + to_f32<T>(res[i + j]));
+      } else if (i + 8 <= hi) {
         *reinterpret_cast<V*>(y + i) = *reinterpret_cast<const V*>(src + i);
-      else
+      } else {
         for (int64_t j = i; j < hi; ++j) y[j] = src[j];
+      }
     }
   }
   __syncthreads();
@@ -289,30 +308,103 @@ __global__ void __launch_bounds__(kThreads) twoshot_kernel(Params2 p, const uint
 }
 
 template <typename T>
-static int launch2(const Params2& p, const void* x, void* y, int64_t n, hipStream_t st) {
+static int launch2(const Params2& p, const void* x, void* y, const void* res, int64_t n,
+                   hipStream_t st) {
   const uint16_t* xi = static_cast<const uint16_t*>(x);
   uint16_t* yo = static_cast<uint16_t*>(y);
+  const uint16_t* ri = static_cast<const uint16_t*>(res);
   switch (p.world) {
-    case 2: twoshot_kernel<T, 2><<<k2Blocks, kThreads, 0, st>>>(p, xi, yo, n); break;
-    case 4: twoshot_kernel<T, 4><<<k2Blocks, kThreads, 0, st>>>(p, xi, yo, n); break;
-    case 8: twoshot_kernel<T, 8><<<k2Blocks, kThreads, 0, st>>>(p, xi, yo, n); break;
+    case 2: twoshot_kernel<T, 2><<<k2Blocks, kThreads, 0, st>>>(p, xi, yo, ri, n); break;
+    case 4: twoshot_kernel<T, 4><<<k2Blocks, kThreads, 0, st>>>(p, xi, yo, ri, n); break;
+    case 8: twoshot_kernel<T, 8><<<k2Blocks, kThreads, 0, st>>>(p, xi, yo, ri, n); break;
     default: return -1;
   }
   return static_cast<int>(hipGetLastError());
 }
 
 template <typename T>
-static int launch(const Params& p, const void* x, void* y, int64_t n, int blocks,
-                  hipStream_t st) {
+static int launch(const Params& p, const void* x, void* y, const void* res, int64_t n,
+                  int blocks, hipStream_t st) {
   const uint16_t* xi = static_cast<const uint16_t*>(x);
   uint16_t* yo = static_cast<uint16_t*>(y);
+  const uint16_t* ri = static_cast<const uint16_t*>(res);
   switch (p.world) {
-    case 2: oneshot_kernel<T, 2><<<blocks, kThreads, 0, st>>>(p, xi, yo, n); break;
-    case 4: oneshot_kernel<T, 4><<<blocks, kThreads, 0, st>>>(p, xi, yo, n); break;
-    case 8: oneshot_kernel<T, 8><<<blocks, kThreads, 0, st>>>(p, xi, yo, n); break;
+    case 2: oneshot_kernel<T, 2><<<blocks, kThreads, 0, st>>>(p, xi, yo, ri, n); break;
+    case 4: oneshot_kernel<T, 4><<<blocks, kThreads, 0, st>>>(p, xi, yo, ri, n); break;
+    case 8: oneshot_kernel<T, 8><<<blocks, kThreads, 0, st>>>(p, xi, yo, ri, n); break;
     default: return -1;
   }
   return static_cast<int>(hipGetLastError());
+}
+
+
+// ---- X4: int64 MAX of the vocab-parallel sampler keys (one tiny block) ------------------
+// Each rank's LM-head shard reduces a decode row to one signed-orderable packed
+// (score, -token) key; the MAX over ranks is the global Gumbel-max winner.  Same push /
+// flag / rank-order protocol as the one-shot kernel, on a region of its own inside the
+// one-shot buffer's header (its own flags, generation counter and 2 x kMaxRanks x kMaxKeys
+// slots), so its single-block generations never interleave with the 32-block sum kernel's.
+// Writes the reduced keys in place and, when tokens != nullptr, the decoded token ids - the
+// step then ends on the device with no torch ops after the collective (graph-capturable).
+constexpr int kMaxKeys = 256;
+constexpr size_t kKeyRegion = 8192;  // byte offset of the max-kernel region in the header
+__device__ __forceinline__ uint32_t* kflag_ptr(uint8_t* base, int par, int src) {
+  return reinterpret_cast<uint32_t*>(base + kKeyRegion) + par * kMaxRanks + src;
+}
+__device__ __forceinline__ long long* kslot_ptr(uint8_t* base, int par, int src) {
+  return reinterpret_cast<long long*>(base + kKeyRegion + 256) + (par * kMaxRanks + src) * kMaxKeys;
+}
+static_assert(kKeyRegion + 256 + 2 * kMaxRanks * kMaxKeys * 8 <= kHeaderBytes, "key region");
+
+template <int W>
+__global__ void __launch_bounds__(kMaxKeys) keymax_kernel(Params p, long long* keys,
+                                                          int64_t* tokens, int n) {
+  uint8_t* mine = p.base[p.rank];
+  uint32_t* counter = reinterpret_cast<uint32_t*>(mine + kKeyRegion) + 2 * kMaxRanks;
+  uint32_t* errw = reinterpret_cast<uint32_t*>(mine + kFlagBytes) + kMaxBlocks;
+  __shared__ uint32_t gen_s;
+  if (threadIdx.x == 0) gen_s = *counter + 1;
+  __syncthreads();
+  const uint32_t gen = gen_s;
+  const int par = gen & 1;
+  const int i = threadIdx.x;
+  long long k = 0;
+  if (i < n) {
+    k = keys[i];
+#pragma unroll
+    for (int q = 0; q < W; ++q) kslot_ptr(p.base[q], par, p.rank)[i] = k;
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x < W) {
+    __hip_atomic_store(kflag_ptr(p.base[threadIdx.x], par, p.rank), gen, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* f = kflag_ptr(mine, par, threadIdx.x);
+    uint32_t spins = 0;  // bounded (~2-4 s): a dead peer sets its bit in the error word
+    while (static_cast<int32_t>(__hip_atomic_load(f, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_SYSTEM) - gen) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 25)) {
+        atomicOr(errw, 1u << threadIdx.x);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+  if (i < n) {
+    long long best = kslot_ptr(mine, par, 0)[i];
+#pragma unroll
+    for (int q = 1; q < W; ++q) {
+      const long long o = kslot_ptr(mine, par, q)[i];
+      best = o > best ? o : best;
+    }
+    keys[i] = best;
+    if (tokens != nullptr)
+      tokens[i] = static_cast<int64_t>(0xFFFFFFFFu - static_cast<unsigned>(best & 0xFFFFFFFFll));
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *counter = gen;
 }
 
 }  // namespace ar
@@ -352,7 +444,7 @@ int64_t atta_ar_error_offset() {
 }
 
 int atta_ar_run(void* const* bases, int rank, int world, int64_t max_elems, const void* x, void* y,
-                int64_t n, int dtype, hipStream_t stream) {
+                const void* res, int64_t n, int dtype, hipStream_t stream) {
   if (world != 2 && world != 4 && world != 8) return -1;
   if (rank < 0 || rank >= world || n <= 0 || n > max_elems) return -1;
   ar::Params p{};
@@ -361,8 +453,24 @@ int atta_ar_run(void* const* bases, int rank, int world, int64_t max_elems, cons
   p.world = world;
   p.max_elems = max_elems;
   // fixed grid (see the generation argument above); blocks past the data only signal
-  return dtype == 0 ? ar::launch<__bf16>(p, x, y, n, ar::kMaxBlocks, stream)
-                    : ar::launch<_Float16>(p, x, y, n, ar::kMaxBlocks, stream);
+  return dtype == 0 ? ar::launch<__bf16>(p, x, y, res, n, ar::kMaxBlocks, stream)
+                    : ar::launch<_Float16>(p, x, y, res, n, ar::kMaxBlocks, stream);
+}
+
+int atta_ar_keymax(void* const* bases, int rank, int world, long long* keys, int64_t* tokens,
+                   int n, hipStream_t stream) {
+  if (world != 2 && world != 4 && world != 8) return -1;
+  if (rank < 0 || rank >= world || n <= 0 || n > ar::kMaxKeys) return -1;
+  ar::Params p{};
+  for (int i = 0; i < world; ++i) p.base[i] = static_cast<uint8_t*>(bases[i]);
+  p.rank = rank;
+  p.world = world;
+  switch (world) {
+    case 2: ar::keymax_kernel<2><<<1, ar::kMaxKeys, 0, stream>>>(p, keys, tokens, n); break;
+    case 4: ar::keymax_kernel<4><<<1, ar::kMaxKeys, 0, stream>>>(p, keys, tokens, n); break;
+    default: ar::keymax_kernel<8><<<1, ar::kMaxKeys, 0, stream>>>(p, keys, tokens, n); break;
+  }
+  return static_cast<int>(hipGetLastError());
 }
 
 // ---- two-shot entry points --------------------------------------------------------------
@@ -383,7 +491,7 @@ int64_t atta_ar2_error_offset() {
 }
 
 int atta_ar2_run(void* const* bases, int rank, int world, int64_t max_elems, const void* x,
-                 void* y, int64_t n, int dtype, hipStream_t stream) {
+                 void* y, const void* res, int64_t n, int dtype, hipStream_t stream) {
   if (world != 2 && world != 4 && world != 8) return -1;
   if (rank < 0 || rank >= world || n <= 0 || n > max_elems) return -1;
   ar::Params2 p{};
@@ -391,6 +499,6 @@ int atta_ar2_run(void* const* bases, int rank, int world, int64_t max_elems, con
   p.rank = rank;
   p.world = world;
   p.chunk_max = chunk_max_of(max_elems, world);
-  return dtype == 0 ? ar::launch2<__bf16>(p, x, y, n, stream)
-                    : ar::launch2<_Float16>(p, x, y, n, stream);
+  return dtype == 0 ? ar::launch2<__bf16>(p, x, y, res, n, stream)
+                    : ar::launch2<_Float16>(p, x, y, res, n, stream);
 }

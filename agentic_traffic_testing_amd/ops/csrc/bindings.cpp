@@ -536,8 +536,16 @@ void ar_close(int64_t ptr) {
   check_rc(atta_ar_ipc_close(reinterpret_cast<void*>(ptr)), "ar_close");
 }
 
+const void* res_ptr(const c10::optional<at::Tensor>& res, const at::Tensor& x, const char* what) {
+  if (!res.has_value()) return nullptr;
+  TORCH_CHECK(res->is_contiguous() && res->numel() == x.numel() &&
+                  res->scalar_type() == x.scalar_type() && res->device() == x.device(),
+              what, ": residual layout");
+  return res->data_ptr();
+}
+
 void ar_run(const at::Tensor& x, at::Tensor y, at::IntArrayRef bases, int64_t rank,
-            int64_t max_elems) {
+            int64_t max_elems, const c10::optional<at::Tensor>& residual) {
   check_dev(x, "x");
   TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel() &&
                   x.scalar_type() == y.scalar_type(), "ar_run: layout");
@@ -546,8 +554,31 @@ void ar_run(const at::Tensor& x, at::Tensor y, at::IntArrayRef bases, int64_t ra
   for (size_t i = 0; i < bases.size(); ++i) b[i] = reinterpret_cast<void*>(bases[i]);
   const at::DeviceGuard g(x.device());
   check_rc(atta_ar_run(b, static_cast<int>(rank), static_cast<int>(bases.size()), max_elems,
-                       x.data_ptr(), y.data_ptr(), x.numel(), dtype_code(x), cur_stream()),
+                       x.data_ptr(), y.data_ptr(), res_ptr(residual, x, "ar_run"), x.numel(),
+                       dtype_code(x), cur_stream()),
            "ar_run");
+}
+
+void ar_keymax(at::Tensor keys, const c10::optional<at::Tensor>& tokens, at::IntArrayRef bases,
+               int64_t rank) {
+  check_dev(keys, "keys");
+  TORCH_CHECK(keys.is_contiguous() && keys.scalar_type() == at::kLong && keys.numel() > 0 &&
+                  keys.numel() <= 256, "ar_keymax: <= 256 contiguous int64 keys");
+  TORCH_CHECK(bases.size() >= 2 && bases.size() <= 8, "ar_keymax: 2..8 ranks");
+  int64_t* tok = nullptr;
+  if (tokens.has_value()) {
+    TORCH_CHECK(tokens->is_contiguous() && tokens->scalar_type() == at::kLong &&
+                    tokens->numel() >= keys.numel() && tokens->device() == keys.device(),
+                "ar_keymax: tokens");
+    tok = tokens->data_ptr<int64_t>();
+  }
+  void* b[8] = {};
+  for (size_t i = 0; i < bases.size(); ++i) b[i] = reinterpret_cast<void*>(bases[i]);
+  const at::DeviceGuard g(keys.device());
+  check_rc(atta_ar_keymax(b, static_cast<int>(rank), static_cast<int>(bases.size()),
+                          reinterpret_cast<long long*>(keys.data_ptr<int64_t>()), tok,
+                          static_cast<int>(keys.numel()), cur_stream()),
+           "ar_keymax");
 }
 
 int64_t ar2_buffer_bytes(int64_t max_elems, int64_t world, int64_t elem_bytes) {
@@ -564,7 +595,7 @@ int64_t ar2_error(int64_t ptr) {
 }
 
 void ar2_run(const at::Tensor& x, at::Tensor y, at::IntArrayRef bases, int64_t rank,
-             int64_t max_elems) {
+             int64_t max_elems, const c10::optional<at::Tensor>& residual) {
   check_dev(x, "x");
   TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel() &&
                   x.scalar_type() == y.scalar_type(), "ar2_run: layout");
@@ -573,7 +604,8 @@ void ar2_run(const at::Tensor& x, at::Tensor y, at::IntArrayRef bases, int64_t r
   for (size_t i = 0; i < bases.size(); ++i) b[i] = reinterpret_cast<void*>(bases[i]);
   const at::DeviceGuard g(x.device());
   check_rc(atta_ar2_run(b, static_cast<int>(rank), static_cast<int>(bases.size()), max_elems,
-                        x.data_ptr(), y.data_ptr(), x.numel(), dtype_code(x), cur_stream()),
+                        x.data_ptr(), y.data_ptr(), res_ptr(residual, x, "ar2_run"), x.numel(),
+                        dtype_code(x), cur_stream()),
            "ar2_run");
 }
 
@@ -588,10 +620,13 @@ TORCH_LIBRARY(atta, m) {
   m.def("ar_open(Tensor handle) -> int", &ar_open);
   m.def("ar_close(int ptr) -> ()", &ar_close);
   m.def("ar_error(int ptr) -> int", &ar_error);
-  m.def("ar_run(Tensor x, Tensor(a!) y, int[] bases, int rank, int max_elems) -> ()");
+  m.def("ar_run(Tensor x, Tensor(a!) y, int[] bases, int rank, int max_elems, "
+        "Tensor? residual=None) -> ()");
+  m.def("ar_keymax(Tensor(a!) keys, Tensor(b!)? tokens, int[] bases, int rank) -> ()");
   m.def("ar2_buffer_bytes(int max_elems, int world, int elem_bytes) -> int", &ar2_buffer_bytes);
   m.def("ar2_error(int ptr) -> int", &ar2_error);
-  m.def("ar2_run(Tensor x, Tensor(a!) y, int[] bases, int rank, int max_elems) -> ()");
+  m.def("ar2_run(Tensor x, Tensor(a!) y, int[] bases, int rank, int max_elems, "
+        "Tensor? residual=None) -> ()");
   m.def("skinny_variant(Tensor(a!) y, Tensor x, Tensor w, int variant) -> ()");
   m.def(
       "attention_decode_v2(Tensor(a!) out, Tensor(b!) part_out, Tensor(c!) part_lse, "
@@ -644,6 +679,7 @@ TORCH_LIBRARY(atta, m) {
 TORCH_LIBRARY_IMPL(atta, CUDA, m) {
   m.impl("ar_run", &ar_run);
   m.impl("ar2_run", &ar2_run);
+  m.impl("ar_keymax", &ar_keymax);
   m.impl("rms_norm", &rms_norm);
   m.impl("fused_add_rms_norm", &fused_add_rms_norm);
   m.impl("silu_and_mul", &silu_and_mul);

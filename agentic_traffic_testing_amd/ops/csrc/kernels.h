@@ -115,12 +115,16 @@ int64_t atta_ar_error_offset();
 int atta_ar_ipc_handle(void* ptr, void* handle_out);
 int atta_ar_ipc_open(const void* handle, void** ptr);
 int atta_ar_ipc_close(void* ptr);
+// res != nullptr: y = res + sum (residual-stream update fused; y may alias res)
 int atta_ar_run(void* const* bases, int rank, int world, int64_t max_elems, const void* x,
-                void* y, int64_t n, int dtype, hipStream_t stream);
+                void* y, const void* res, int64_t n, int dtype, hipStream_t stream);
+// X4: in-place int64 MAX of n <= 256 sampler keys (+ decoded token ids when tokens != null)
+int atta_ar_keymax(void* const* bases, int rank, int world, long long* keys, int64_t* tokens,
+                   int n, hipStream_t stream);
 
 // ---- two-shot IPC all-reduce (allreduce.hip): reduce-scatter + all-gather ----------------
 size_t atta_ar2_buffer_bytes(int64_t max_elems, int world, int elem_bytes);
 int64_t atta_ar2_error_offset();
 int atta_ar2_run(void* const* bases, int rank, int world, int64_t max_elems, const void* x,
-                 void* y, int64_t n, int dtype, hipStream_t stream);
+                 void* y, const void* res, int64_t n, int dtype, hipStream_t stream);
 

@@ -51,6 +51,22 @@ class TPComm:
         dist.all_reduce(x, group=self.group)
         return x
 
+    def all_reduce_residual(self, x: torch.Tensor, residual: torch.Tensor) -> torch.Tensor:
+        """``residual += all_reduce(x)`` (row-parallel o / down projections).  On the IPC
+        path the add is the reduction kernel's epilogue: no extra launch or HBM pass."""
+        if self.size == 1:
+            return residual.add_(x)
+        if self.ipc is not None and self.ipc.eligible(x):
+            return self.ipc.all_reduce(x, residual=residual)
+        return residual.add_(self.all_reduce(x))
+
+    @property
+    def decode_capturable(self) -> bool:
+        """Can a decode step's collectives (X1/X2 sums, X4 key MAX) be hipGraph-captured?
+        RCCL: yes.  gloo (a same-GPU rehearsal's control group): only when the IPC kernels
+        carry them - then the whole step stays on the device."""
+        return self.size == 1 or not self.is_gloo or self.ipc is not None
+
     def _gloo_inplace(self, x: torch.Tensor, op) -> torch.Tensor:
         tmp = x.float() if x.dtype in (torch.bfloat16, torch.float16) else x
         tmp = tmp.cpu() if tmp.is_cuda else tmp
@@ -62,12 +78,19 @@ class TPComm:
         return x
 
     # -- X4 ---------------------------------------------------------------------------------
-    def all_reduce_max(self, x: torch.Tensor) -> torch.Tensor:
+    def all_reduce_max(self, x: torch.Tensor, tokens: torch.Tensor | None = None) -> torch.Tensor:
+        """In-place MAX.  For sampler keys with ``tokens``, the decoded winners are written
+        there too (IPC path: by the reduction kernel itself)."""
         if self.size == 1:
-            return x
-        if self.is_gloo:
-            return self._gloo_inplace(x, dist.ReduceOp.MAX)
-        dist.all_reduce(x, op=dist.ReduceOp.MAX, group=self.group)
+            pass
+        elif self.ipc is not None and self.ipc.keys_eligible(x):
+            return self.ipc.all_reduce_max_keys(x, tokens)
+        elif self.is_gloo:
+            self._gloo_inplace(x, dist.ReduceOp.MAX)
+        else:
+            dist.all_reduce(x, op=dist.ReduceOp.MAX, group=self.group)
+        if tokens is not None:
+            tokens[:x.shape[0]].copy_(0xFFFFFFFF - (x & 0xFFFFFFFF))
         return x
 
     def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:

@@ -90,6 +90,7 @@ class IpcAllReduce:
         comm.barrier()  # every rank mapped every buffer before the first kernel
         self.calls = 0
         self.calls2 = 0
+        self.calls_max = 0
 
     def _ok(self, x: torch.Tensor) -> bool:
         return (x.is_cuda and x.is_contiguous() and x.dtype in (torch.bfloat16, torch.float16)
@@ -98,22 +99,41 @@ class IpcAllReduce:
     def eligible(self, x: torch.Tensor) -> bool:
         return self._ok(x) and (x.numel() <= self.max_elems or x.numel() <= self.max_elems2)
 
-    def all_reduce(self, x: torch.Tensor, mode: str = "auto") -> torch.Tensor:
-        """In-place sum over the TP ranks.  ``mode``: auto | oneshot | twoshot."""
+    def all_reduce(self, x: torch.Tensor, mode: str = "auto",
+                   residual: torch.Tensor | None = None) -> torch.Tensor:
+        """Sum over the TP ranks, in place in ``x`` - or, with ``residual``, the residual-stream
+        update ``residual += sum`` fused into the reduction's epilogue (returns residual).
+        ``mode``: auto | oneshot | twoshot."""
         n = x.numel()
+        y = x if residual is None else residual
         two = mode == "twoshot" or (mode == "auto" and (
             n > self.max_elems or n * self.elem > ONESHOT_MAX_BYTES) and n <= self.max_elems2)
         if two:
             if self.large is None or n > self.max_elems2:
                 raise ValueError("message larger than the two-shot buffer")
-            self._ops.ar2_run(x, x, self.large.bases, self.comm.rank, self.max_elems2)
+            self._ops.ar2_run(x, y, self.large.bases, self.comm.rank, self.max_elems2, residual)
             self.calls2 += 1
         else:
             if n > self.max_elems:
                 raise ValueError("message larger than the one-shot buffer")
-            self._ops.ar_run(x, x, self.bases, self.comm.rank, self.max_elems)
+            self._ops.ar_run(x, y, self.bases, self.comm.rank, self.max_elems, residual)
             self.calls += 1
-        return x
+        return y
+
+    MAX_KEYS = 256
+
+    def keys_eligible(self, keys: torch.Tensor) -> bool:
+        return (keys.is_cuda and keys.is_contiguous() and keys.dtype == torch.int64
+                and 0 < keys.numel() <= self.MAX_KEYS)
+
+    def all_reduce_max_keys(self, keys: torch.Tensor,
+                            tokens: torch.Tensor | None = None) -> torch.Tensor:
+        """X4: in-place int64 MAX of the vocab-parallel sampler keys over the TP ranks (one
+        tiny kernel on the one-shot peer buffers); with ``tokens`` the winners' token ids are
+        written there by the same kernel."""
+        self._ops.ar_keymax(keys, tokens, self.bases, self.comm.rank)
+        self.calls_max += 1
+        return keys
 
     def check(self) -> int:
         """Error words: bit q set = a wait for rank q timed out (one-shot | two-shot)."""

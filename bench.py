@@ -87,6 +87,9 @@ def parse_args(argv=None):
                     help="EngineConfig override for A/B runs (e.g. fuse_attn_oproj=0)")
     ap.add_argument("--parallel", choices=["dp", "tp"], default="dp",
                     help="dp: one engine replica per GPU (default); tp: one engine over all GPUs")
+    ap.add_argument("--tp-same-device", action="store_true",
+                    help="--parallel tp rehearsal with every rank on cuda:0 (IPC collectives, "
+                         "graph-captured decode): the TP protocol on a one-GPU box")
     ap.add_argument("--via", choices=["engine", "http"], default="engine",
                     help="engine: drive the engine in-process (headline); http: the whole "
                          "serving stack - aiohttp llm-backend + Agent A + 5 Agent B over "
@@ -105,7 +108,7 @@ def self_launch(a) -> int:
 
     Runs before this process makes any GPU call (device_count() does not initialise HIP on
     this image), so no exec happens from a GPU-initialised process."""
-    if a.device == "cuda":
+    if a.device == "cuda" and not a.tp_same_device:
         have = torch.cuda.device_count()
         if have < a.gpus:
             print(json.dumps({"metric": METRIC, "error": f"--gpus {a.gpus} requested but only "
@@ -326,7 +329,8 @@ def main_tp(a):
     world = int(os.environ["WORLD_SIZE"])
     rank = int(os.environ.get("RANK", "0"))
     dev = "cuda" if a.device == "cuda" else "cpu"
-    cfg = _cfg(a, dev, tensor_parallel_size=world)
+    kw = dict(tp_same_device=True, tp_allreduce="ipc") if a.tp_same_device else {}
+    cfg = _cfg(a, dev, tensor_parallel_size=world, **kw)
     port = int(os.environ.get("MASTER_PORT", "29511"))
     if rank > 0:
         from agentic_traffic_testing_amd.parallel.tp_engine import run_worker
@@ -364,7 +368,9 @@ def main_tp(a):
         "config": {"model": f"{label} (random-init)", "global_batch": a.fanout,
                    "seq_len": a.max_model_len, "parallelism": f"tp{world}",
                    "max_tokens": a.max_tokens, "hipgraphs": cfg.use_graphs,
-                   "tp_allreduce": cfg.tp_allreduce, "device": a.device},
+                   "tp_allreduce": cfg.tp_allreduce, "device": a.device,
+                   "tp_same_device": cfg.tp_same_device},
+        "graph_steps": eng.runner.graph_steps, "steps_total": eng.runner.steps,
         "p50_ttft_s": round(statistics.median(ttfts), 4) if ttfts else None,
         "p95_ttft_s": round(ttfts[min(len(ttfts) - 1, int(0.95 * len(ttfts)))], 4)
         if ttfts else None,

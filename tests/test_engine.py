@@ -216,6 +216,44 @@ def test_special_sampling_graphs_equal_eager():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("case", ["bucket64", "unfused_special"])
+def test_unfused_graph_buckets_equal_eager(case):
+    """graph replays of the non-fused decode path must leave the sampled
+    tokens in ws["tokens"] (where launch() reads them and the look-ahead step embeds them).
+    bucket64: 40 sequences replay the 64-bucket graph, past the fused GEMV limit (32 rows),
+    so the step is forward() + LM head + sampler; unfused_special: max_model_len 20000 turns
+    the fused decode path off and every row uses top-p / top-k.  Graph == eager, token for
+    token."""
+    rng = np.random.default_rng(21)
+    if case == "bucket64":
+        prompts = [rng.integers(300, 30000, size=int(n)).tolist()
+                   for n in rng.integers(5, 60, size=40)]
+        sp = [SamplingParams(temperature=0.7, max_tokens=6, ignore_eos=True, seed=300 + i)
+              for i in range(40)]
+        kw = dict(max_model_len=512, num_kv_blocks=1024, max_num_seqs=40,
+                  max_num_batched_tokens=4096, graph_batch_sizes=(1, 2, 4, 8, 16, 32, 64))
+    else:
+        prompts = _prompts(vocab=30000)
+        sp = _special_params(len(prompts))
+        kw = dict(max_model_len=20000, num_kv_blocks=512, max_num_seqs=8,
+                  graph_batch_sizes=(1, 2, 4, 8))
+    res = []
+    for graphs in (False, True):
+        eng = LLMEngine(EngineConfig(model="small", device="cuda", use_graphs=graphs, **kw))
+        if case == "unfused_special":
+            assert not eng.runner.fused_decode
+        outs = eng.generate(prompts, sp)
+        res.append([o.token_ids for o in outs])
+        if graphs:
+            assert eng.runner.graph_steps > 0
+            if case == "bucket64":
+                assert any(k[0] == 64 for k in eng.runner.graphs), sorted(eng.runner.graphs)
+        del eng
+        torch.cuda.empty_cache()
+    assert res[0] == res[1]
+
+
+@pytest.mark.gpu
 def test_fp8_engine_gpu():
     """fp8 weights end to end: graph decode == eager decode, and the fp8 model's greedy
     tokens mostly agree with the dense oracle over the dequantised weights."""

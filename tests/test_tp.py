@@ -229,11 +229,10 @@ def test_shm_channel_registration_deadline():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("allreduce", ["auto", "ipc"])
-def test_tp2_same_gpu_rehearsal(allreduce):
-    """Two TP ranks on ONE MI355X (gloo control + host-staged collectives, since RCCL
-    refuses duplicate devices): exercises the fused decode path's vocab-parallel sampler
-    (finalize="key" + MAX all-reduce) and the step-channel protocol on real kernels."""
+def test_tp2_same_gpu_rehearsal_host_collectives():
+    """Two TP ranks on ONE MI355X with the host-staged gloo collectives (RCCL refuses
+    duplicate devices; tp_allreduce=auto installs no IPC there): eager steps, the fused decode
+    path's vocab-parallel sampler and the step-channel protocol on real kernels."""
     base = dict(model="small", device="cuda:0", max_model_len=512, num_kv_blocks=256,
                 max_num_batched_tokens=256, max_num_seqs=4, use_graphs=False)
     greedy = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
@@ -241,20 +240,55 @@ def test_tp2_same_gpu_rehearsal(allreduce):
     exp = [o.token_ids for o in ref_eng.generate(_prompts(), greedy)]
     del ref_eng
     torch.cuda.empty_cache()
-    eng = TPEngine(EngineConfig(tensor_parallel_size=2, tp_same_device=True,
-                                tp_allreduce=allreduce, **base))
+    eng = TPEngine(EngineConfig(tensor_parallel_size=2, tp_same_device=True, **base))
     try:
         got = [o.token_ids for o in eng.generate(_prompts(), greedy)]
-        # top-k / top-p on real kernels: every rank samples the all-gathered logits
         topp = SamplingParams(temperature=0.7, top_p=0.9, top_k=40, max_tokens=4,
                               ignore_eos=True, seed=5)
         assert all(len(o.token_ids) == 4 for o in eng.generate(_prompts()[:2], topp))
-        if allreduce == "ipc":
-            assert eng.comm.ipc is not None and eng.comm.ipc.calls > 0
-            assert eng.comm.ipc.check() == 0
+        assert eng.comm.ipc is None and eng.runner.graph_steps == 0
     finally:
         eng.shutdown()
     # bf16 partial sums split across ranks round differently: allow a late near-tie flip
+    assert all(g[:2] == e[:2] for g, e in zip(got, exp)), (got, exp)
+    assert sum(g == e for g, e in zip(got, exp)) >= 2, (got, exp)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tp,model", [(2, "small"), (4, "llama-70b-tp-slice"),
+                                      (8, "llama-70b-tp-slice")])
+def test_tp_same_gpu_graph_captured_decode(tp, model):
+    """TP=2/4/8 on ONE MI355X with hipGraph-captured decode.  Every decode-step
+    collective is an IPC kernel on the peer buffers (X1/X2 sums with the residual add fused
+    into the epilogue, X4 sampler-key MAX writing the token ids), so the whole step - every
+    rank's 5 kernels x layers + 2 all-reduces per layer + LM head + key MAX - is captured and
+    replayed although the control group is gloo.  Greedy tokens equal TP=1's (graphs on) up to
+    a late bf16 near-tie flip; the IPC timeout word stays 0."""
+    base = dict(model=model, device="cuda:0", max_model_len=512, num_kv_blocks=128,
+                max_num_batched_tokens=256, max_num_seqs=4, use_graphs=True)
+    greedy = SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True)
+    ref_eng = LLMEngine(EngineConfig(**base))
+    exp = [o.token_ids for o in ref_eng.generate(_prompts(), greedy)]
+    assert ref_eng.runner.graph_steps > 0
+    del ref_eng
+    torch.cuda.empty_cache()
+    eng = TPEngine(EngineConfig(tensor_parallel_size=tp, tp_same_device=True,
+                                tp_allreduce="ipc", **base))
+    try:
+        r = eng.runner
+        assert eng.comm.decode_capturable and r.graphs, "no decode graph was captured"
+        steps0 = r.graph_steps
+        got = [o.token_ids for o in eng.generate(_prompts(), greedy)]
+        assert r.graph_steps > steps0, "TP decode steps did not replay from graphs"
+        sampled = SamplingParams(temperature=0.8, max_tokens=6, ignore_eos=True, seed=9)
+        s1 = [o.token_ids for o in eng.generate(_prompts(), sampled)]
+        s2 = [o.token_ids for o in eng.generate(_prompts(), sampled)]
+        assert s1 == s2  # seeded Gumbel draws: replay-deterministic across the TP group
+        ipc = eng.comm.ipc
+        assert ipc.calls > 0 and ipc.calls_max > 0
+        assert ipc.check() == 0
+    finally:
+        eng.shutdown()
     assert all(g[:2] == e[:2] for g, e in zip(got, exp)), (got, exp)
     assert sum(g == e for g, e in zip(got, exp)) >= 2, (got, exp)
 
