@@ -102,6 +102,12 @@ MODEL_PRESETS: dict[str, ModelConfig] = {
                                   num_kv_heads=8, tie_word_embeddings=True,
                                   rope_scaling=dict(LLAMA3_ROPE_SCALING, factor=32.0),
                                   bos_token_id=16000, eos_token_ids=(16001, 16009)),
+    # the Llama-3.1-8B layer geometry (hidden 4096, 32 q / 8 kv heads, FFN 14336) with 2
+    # layers and a small vocab: the persistent decode step's shapes on one GPU in seconds
+    "llama-8b-slice": ModelConfig(name="llama-8b-slice", vocab_size=16384, hidden_size=4096,
+                                  intermediate_size=14336, num_layers=2, num_heads=32,
+                                  num_kv_heads=8, max_position_embeddings=16384,
+                                  bos_token_id=16000, eos_token_ids=(16001, 16009)),
     # the Llama-3-70B TP=8 per-rank geometry (one KV head and 8 q heads per rank, hidden 8192)
     # with an FFN that stays fused-decode-shaped at TP=2/4/8 (7168 / 8 = 896 = 7 x 128): the
     # one-GPU TP rehearsal of graph-captured decode
@@ -199,6 +205,9 @@ class EngineConfig:
     long_prefill_token_threshold: int = 0
     # fused native decode path (GEMV kernels) when available
     fused_decode: bool = True
+    # whole decode step as ONE persistent launch (ops/csrc/decode_step.hip): TP = 1 bf16
+    # models whose shapes it covers, decode batches <= decode_small_batch_max rows
+    decode_megakernel: bool = False
     # async look-ahead decode: launch the next decode graph step before waiting for the
     # current one's tokens (llm_engine.LLMEngine.step)
     async_decode: bool = True

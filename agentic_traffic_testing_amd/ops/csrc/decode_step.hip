@@ -1,0 +1,1014 @@
+// Persistent decode step: the WHOLE decode forward of a Llama-3 model (embedding, every
+// layer's [norm+QKV+RoPE+KV write] -> [paged attention] -> [o_proj + residual] ->
+// [norm+gate_up+SiLU*up] -> [down + residual], final norm + LM head + Gumbel-max sampler)
+// in ONE launch (VERDICT r2 "break the ~3.0 ms decode floor").
+//
+// Why.  A bf16 decode step of Llama-3.1-8B at B <= 5 streams 15 GB of weights; as 160+
+// dependent launches every kernel pays its ramp and tail (~4 us: the read-only launch chain
+// of the same bytes takes 2.84 ms against 2.30 ms for one monolithic read,
+// profiles/r2_decode_roofline.md) and the latency-bound attention (~9 us/layer) leaves HBM
+// idle.  Here each CU's weight bytes for the entire step form ONE stream that never waits
+// for a dependency: a loader wave copies them by LDS-DMA into a 128 KiB ring ahead of the
+// compute waves, across phase boundaries and through the attention phase; only the
+// compute waves wait for the previous phase's results.
+//
+// Structure (one 576-thread workgroup per CU, grid = #CUs, all co-resident):
+//   * waves 0-7 compute, wave 8 loads.  A GEMV phase hands every workgroup the 16-row
+//     output tiles t = blockIdx.x + i * G; the 8 compute waves split each tile's K into 8
+//     slices; a wave's slice is consumed in 8 KiB chunks (8 MFMA blocks of 16 rows x 32 k,
+//     the pre-shuffled layout of ops.preshuffle: one contiguous 1 KiB per block).
+//   * ring: 16 slots of 8 KiB, slot = seq & 15 for the workgroup's chunk sequence; chunk
+//     seq is consumed by wave seq & 7, so each wave owns two alternating slots.  FULL /
+//     FREE generation words in LDS: the loader publishes a slot behind a counted vmcnt that
+//     keeps the next two chunks in flight; a wave releases a slot as soon as its 8 KiB are
+//     in registers (before the MFMAs).
+//   * activations (x) are read by the compute waves straight from global memory with
+//     device-scope (sc1) buffer loads, one chunk ahead; the norm's sum of squares comes from
+//     the same fragments.  Waves combine their K-slice partials through LDS; epilogues
+//     (RoPE + q / K / V-cache writes, residual add, SiLU*up, sampler keys) store sc1.
+//   * phase hand-offs (MI355X_MICROARCH.md Valid forms, row 1): every storing wave drains
+//     (s_waitcnt vmcnt(0)), the compute waves meet in an LDS barrier, one lane adds to the
+//     phase's arrival counter (8 per-XCD shards on their own 64-B lines); the next phase's
+//     wave 0 polls the shards relaxed, then every handed-off byte is read with sc1 loads.
+//     No s_barrier anywhere: the loader wave never joins a barrier, the compute waves sync
+//     through LDS.  Counters are re-zeroed in flight (C[p-2] once everyone passed poll p)
+//     and by the last workgroup to finish, so a graph replay needs no memset node.
+//   * every spin is bounded: a timeout sets a bit in the error word (ops.decode_step_error)
+//     and the kernel runs on to its end - a broken hand-off yields garbage, never a hang.
+//   * attention: units (sequence, KV head, 128-token partition) round-robin over the
+//     workgroups, one 16-token tile per compute wave, split-K combine by the last arriving
+//     partition (the attention_decode.hip scheme), all KV / q loads sc1 (the current
+//     token's K/V were written in this launch).
+//
+// Scope: TP = 1, 16-bit pre-shuffled weights, K dims multiples of 2048 (H, I, NQ*128),
+// GQA group <= 4, <= 16 rows, 128-token partitions; the model runner falls back to the
+// per-kernel decode path otherwise.
+#include <map>
+#include <mutex>
+#include <string>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace atta {
+namespace mk {
+
+constexpr int kCW = 8;                    // compute waves
+constexpr int kThreads = (kCW + 1) * 64;  // + the loader wave
+constexpr int kSlots = 16;                // ring slots (2 per compute wave)
+constexpr int kSlotBytes = 8192;          // 8 MFMA blocks of 1 KiB
+constexpr int kRows = 16;                 // MFMA M (rows >= p.M are zero)
+constexpr int kD = 128;
+constexpr int kShards = 8;
+constexpr int kCtrStride = 16;            // uint32 words between counter shards (64 B)
+constexpr int kMaxG = 4;                  // GQA group
+constexpr int kPartTokens = kCW * 16;     // attention partition = 8 waves x 16 tokens
+constexpr unsigned kSpinLimit = 1u << 24;
+
+// error word bits
+constexpr unsigned kErrPoll = 1u, kErrFull = 2u, kErrFree = 4u, kErrBar = 8u;
+
+struct LayerW {
+  const uint16_t* qkv;
+  const uint16_t* o;
+  const uint16_t* gu;
+  const uint16_t* down;
+};
+
+struct Params {
+  int M, H, I, V, L, NQ, NKV, G;
+  int bt_stride, bs_shift, max_parts;
+  float eps, scale_log2;
+  const LayerW* layers;
+  const uint16_t* lm_head;
+  const uint16_t* embed;
+  uint16_t* k_cache;
+  uint16_t* v_cache;
+  int64_t cache_layer_elems;
+  const int* input_ids;
+  const int64_t* prev_tokens;
+  const int* feed_prev;
+  const int* positions;
+  const int* slots;
+  const int* block_tables;
+  const int* seq_kvlen;
+  const float* cos_sin;
+  const float* temperature;
+  const int64_t* seeds;
+  const int64_t* steps;
+  uint16_t* x;     // residual stream [M, H]
+  uint16_t* q;     // [M, NQ * 128]
+  uint16_t* attn;  // [M, NQ * 128]
+  uint16_t* act;   // [M, I]
+  float* part_out;
+  float* part_lse;
+  int* att_counters;
+  unsigned long long* keys;  // [M, V / 16]
+  int64_t* tokens;
+  unsigned* sync;  // [NP][kShards][kCtrStride] counters, final counter, error word
+};
+
+enum Kind { K_QKV = 0, K_ATT = 1, K_O = 2, K_GU = 3, K_DOWN = 4 };
+
+// ---- LDS layout ------------------------------------------------------------------------
+struct Red {  // per-tile cross-wave reduction (double-buffered)
+  float acc[2][kCW][kRows][17];
+  float ss[2][kCW][kRows];
+};
+struct AttS {  // attention scratch
+  float o[kCW][kMaxG][kD + 4];
+  float m[kCW][kMaxG];
+  float l[kCW][kMaxG];
+};
+struct MergeS {
+  float mg[8][10][kMaxG * 16];
+};
+union Scratch {
+  Red red;
+  AttS att;
+  MergeS mrg;
+};
+struct Shared {
+  uint8_t ring[kSlots * kSlotBytes];
+  Scratch s;
+  unsigned full[kSlots];
+  unsigned freed[kSlots];
+  unsigned bar_count, bar_gen;
+  int bcast;
+};
+
+// Opaque copy of the parameter-block pointer: loads through it cannot be hoisted across the
+// call, so each phase re-reads the few fields it needs (cheap scalar loads from the kernarg
+// segment) instead of the whole block staying live in SGPRs across the layer loop.
+typedef const __attribute__((address_space(4))) Params* PP;  // constant address space:
+                                                              // scalar (s_load) reads
+__device__ __forceinline__ PP fresh(PP p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+// Same for the LDS block: per-lane LDS addresses derived from a laundered base are computed
+// inside the phase that uses them instead of being hoisted to the kernel entry (where dozens of
+// them stay live across the layer loop and spill).
+__device__ __forceinline__ Shared& fresh_lds(Shared& s) {
+  __attribute__((address_space(3))) Shared* p = (__attribute__((address_space(3))) Shared*)&s;
+  asm volatile("" : "+s"(p));
+  return *(Shared*)p;
+}
+
+__device__ __forceinline__ unsigned ld_volatile(const unsigned* p) {
+  return *reinterpret_cast<const volatile unsigned*>(p);
+}
+
+// ---- software barrier of the 8 compute waves (LDS; the loader wave never joins) ----------
+__device__ __forceinline__ void cbar(Shared& sh, unsigned* err) {
+  const int lane = threadIdx.x & 63;
+  if (lane == 0) {
+    const unsigned g = ld_volatile(&sh.bar_gen);
+    const unsigned old = atomicAdd(&sh.bar_count, 1u);
+    if (old == kCW - 1) {
+      sh.bar_count = 0;
+      __atomic_fetch_add(&sh.bar_gen, 1u, __ATOMIC_RELEASE);
+    } else {
+      unsigned spins = 0;
+      while (ld_volatile(&sh.bar_gen) == g) {
+        __builtin_amdgcn_s_sleep(0);
+        if (++spins > kSpinLimit) {
+          atomicOr(err, kErrBar);
+          break;
+        }
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// ---- global phase counters ----------------------------------------------------------------
+template <typename P>
+__device__ __forceinline__ unsigned* ctr(const P& p, int phase) {
+  return p.sync + static_cast<int64_t>(phase) * kShards * kCtrStride;
+}
+template <typename P>
+__device__ __forceinline__ unsigned* err_word(const P& p, int np) {
+  return p.sync + static_cast<int64_t>(np) * kShards * kCtrStride + kCtrStride;
+}
+template <typename P>
+__device__ __forceinline__ unsigned* final_word(const P& p, int np) {
+  return p.sync + static_cast<int64_t>(np) * kShards * kCtrStride;
+}
+
+// wave 0 (all lanes) polls the 8 shards of C[phase] until every workgroup arrived
+template <typename P>
+__device__ __forceinline__ void poll_phase(const P& p, int phase, unsigned* err) {
+  const int lane = threadIdx.x & 63;
+  unsigned* c = ctr(p, phase);
+  const unsigned want = lane < kShards ? static_cast<unsigned>((p.G - lane + kShards - 1) / kShards) : 0u;
+  for (unsigned spins = 0;; ++spins) {
+    const unsigned v = lane < kShards ? __hip_atomic_load(c + lane * kCtrStride, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                      : 0u;
+    if (__all(v >= want)) break;
+    if (spins > kSpinLimit) {
+      if (lane == 0) atomicOr(err, kErrPoll);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+template <typename P>
+__device__ __forceinline__ void zero_phase(const P& p, int phase) {
+  const int lane = threadIdx.x & 63;
+  if (lane < kShards)
+    __hip_atomic_store(ctr(p, phase) + lane * kCtrStride, 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// every compute wave drains its stores, the waves meet, one lane arrives
+template <typename P>
+__device__ __forceinline__ void arrive_phase(const P& p, Shared& sh, int phase,
+                                             unsigned* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  cbar(sh, err);
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(ctr(p, phase) + (blockIdx.x & (kShards - 1)) * kCtrStride, 1u,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---- the weight stream ------------------------------------------------------------------
+struct StreamPhase {
+  const uint16_t* w;
+  int K, ntiles;
+};
+template <typename P>
+__device__ __forceinline__ StreamPhase stream_phase(const P& p, int sp) {
+  if (sp >= 4 * p.L) return {p.lm_head, p.H, p.V / 16};
+  const LayerW* lw = p.layers + (sp >> 2);
+  typedef const __attribute__((address_space(4))) LayerW* LWP;
+  const LWP lc = (LWP)lw;
+  switch (sp & 3) {
+    case 0: return {lc->qkv, p.H, (p.NQ + 2 * p.NKV) * 8};
+    case 1: return {lc->o, p.NQ * kD, p.H / 16};
+    case 2: return {lc->gu, p.H, p.I / 8};
+    default: return {lc->down, p.I, p.H / 16};
+  }
+}
+__device__ __forceinline__ int tiles_of(int ntiles, int c, int G) {
+  return ntiles > c ? (ntiles - 1 - c) / G + 1 : 0;
+}
+
+// LDS-DMA: 64 lanes x 16 B from per-lane global addresses into lds_dst + 16 * lane (nt: every
+// weight byte is read once per step by one CU)
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_dst)
+      : "memory");
+}
+
+__device__ void loader(PP pp, Shared& sh, unsigned* err) {
+  const auto& p = *pp;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x;
+  const uint32_t ring0 = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sh.ring)));
+  uint32_t seq = 0;
+  auto publish = [&](uint32_t s) {
+    __atomic_store_n(&sh.full[s & (kSlots - 1)], (s >> 4) + 1, __ATOMIC_RELAXED);
+  };
+  const int nsp = 4 * p.L + 1;
+  for (int sp = 0; sp < nsp; ++sp) {
+    const StreamPhase ph = stream_phase(p, sp);
+    const int nt = tiles_of(ph.ntiles, c, p.G);
+    const int nb = ph.K / 256;  // blocks per wave slice
+    const int nch = nb / 8;
+    const int64_t tile_elems = static_cast<int64_t>(ph.K) * 16;
+    for (int i = 0; i < nt; ++i) {
+      const uint16_t* tb = ph.w + static_cast<int64_t>(c + i * p.G) * tile_elems;
+      for (int j = 0; j < nch; ++j) {
+        for (int w = 0; w < kCW; ++w) {
+          const int slot = seq & (kSlots - 1);
+          const unsigned gen = (seq >> 4) + 1;
+          if (gen > 1) {
+            unsigned spins = 0;
+            while (ld_volatile(&sh.freed[slot]) + 1 < gen) {
+              __builtin_amdgcn_s_sleep(0);
+              if (++spins > kSpinLimit) {
+                atomicOr(err, kErrFree);
+                break;
+              }
+            }
+          }
+          const uint16_t* src = tb + (static_cast<int64_t>(w * nb + j * 8) * 512) + lane * 8;
+          const uint32_t dst = __builtin_amdgcn_readfirstlane(ring0 + slot * kSlotBytes);
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            dma16(src + u * 512, __builtin_amdgcn_readfirstlane(dst + u * 1024));
+          if (seq >= 2) {
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            publish(seq - 2);
+          }
+          ++seq;
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (seq >= 2) publish(seq - 2);
+  if (seq >= 1) publish(seq - 1);
+}
+
+// ---- compute-wave GEMV phase ----------------------------------------------------------------
+typedef bf16x8 frag8;
+
+__device__ __forceinline__ float sq8(frag8 a, float s) {
+  const u32x4 w = __builtin_bit_cast(u32x4, a);
+  f32x2_t acc = {0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f32x2_t v = {__uint_as_float(w[j] << 16), __uint_as_float(w[j] & 0xffff0000u)};
+    acc = __builtin_elementwise_fma(v, v, acc);
+  }
+  return s + (acc[0] + acc[1]);
+}
+
+__device__ __forceinline__ float bf(uint16_t b) { return __uint_as_float(static_cast<uint32_t>(b) << 16); }
+__device__ __forceinline__ uint16_t tobf(float f) { return from_f32<__bf16>(f); }
+
+__device__ __forceinline__ unsigned ordered_bits(float f) {
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float gumbel(uint64_t seed, uint64_t step, uint32_t idx) {
+  const uint64_t h = mix64(seed ^ mix64(step * 0x100000001B3ull + idx));
+  const float u = (static_cast<float>(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
+  return -__logf(-__logf(u));
+}
+
+struct XSrc {  // where the A operand (activation rows) of a GEMV phase comes from
+  __amdgpu_buffer_rsrc_t rs;
+  int64_t row_stride;   // elements
+  bool embed;           // layer-0 QKV: rows of the embedding table (plain loads)
+  const uint16_t* erow;  // this lane's embedding row (embed only)
+};
+
+template <int KIND>
+__device__ void gemv_phase(PP pp, Shared& sh_, int layer, const XSrc& xs,
+                           uint32_t& seq, unsigned* err) {
+  const auto& p = *fresh(pp);
+  Shared& sh = fresh_lds(sh_);
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = lane & 15, grp = lane >> 4;
+  const int c = blockIdx.x;
+  const int sp = KIND == 5 ? 4 * p.L : 4 * layer + (KIND == K_QKV ? 0 : KIND == K_O ? 1 : KIND == K_GU ? 2 : 3);
+  const StreamPhase ph = stream_phase(p, sp);
+  const int nt = tiles_of(ph.ntiles, c, p.G);
+  const int nb = ph.K / 256;
+  const int nch = nb / 8;
+  constexpr bool norm = (KIND == K_QKV || KIND == K_GU || KIND == 5);
+  const bool rowok = col < p.M;
+  const int kw0 = w * nb * 32;  // first k of this wave's slice
+  // x fragment loads of chunk j (this lane: row col, k-group grp)
+  auto load_x = [&](frag8 (&xf)[8], int j) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = kw0 + j * 256 + u * 32 + 8 * grp;
+      if (!rowok) {
+        xf[u] = frag8{};
+      } else if (xs.embed) {
+        xf[u] = *reinterpret_cast<const frag8*>(xs.erow + k);
+      } else {
+        const uint32_t off = static_cast<uint32_t>((col * xs.row_stride + k) * 2);
+        xf[u] = __builtin_bit_cast(frag8, dev_load16(xs.rs, off));
+      }
+    }
+  };
+  for (int i = 0; i < nt; ++i) {
+    const int tile = c + i * p.G;
+    const int tb = i & 1;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    float ss = 0.f;
+    for (int j = 0; j < nch; ++j) {
+      // x fragments of this chunk first (L2 latency overlaps the FULL wait / weight reads;
+      // the compute waves consume ~8x faster than one loader wave streams, so nothing is
+      // gained by holding a second chunk of x in registers)
+      frag8 xa[8];
+      load_x(xa, j);
+      const int slot = seq & (kSlots - 1);
+      const unsigned gen = (seq >> 4) + 1;
+      if (lane == 0) {
+        unsigned spins = 0;
+        while (ld_volatile(&sh.full[slot]) < gen) {
+          __builtin_amdgcn_s_sleep(0);
+          if (++spins > kSpinLimit) {
+            atomicOr(err, kErrFull);
+            break;
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      const uint8_t* sb = sh.ring + slot * kSlotBytes + lane * 16;
+      frag8 wf[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) wf[u] = *reinterpret_cast<const frag8*>(sb + u * 1024);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) __atomic_store_n(&sh.freed[slot], gen, __ATOMIC_RELAXED);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[u], wf[u], acc, 0, 0, 0);
+        if (norm && i == 0) ss = sq8(xa[u], ss);
+      }
+      seq += kCW;
+    }
+    // ---- cross-wave reduction ----------------------------------------------------------
+    Red& r = sh.s.red;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = 4 * grp + e;
+      if (m < p.M) r.acc[tb][w][m][col] = acc[e];
+    }
+    if (norm && i == 0) {
+      ss += __shfl_xor(ss, 16, kWave);
+      ss += __shfl_xor(ss, 32, kWave);
+      if (grp == 0 && rowok) r.ss[0][w][col] = ss;
+    }
+    cbar(sh, err);
+    // ---- epilogue (threads e < outputs of the tile) ----------------------------------------
+    const int e = threadIdx.x;
+    auto inv_rms = [&](int m) {
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < kCW; ++q) s += r.ss[0][q][m];
+      return rsqrtf(s / static_cast<float>(ph.K) + p.eps);
+    };
+    auto red_sum = [&](int m, int n) {
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < kCW; ++q) s += r.acc[tb][q][m][n];
+      return s;
+    };
+    if constexpr (KIND == K_O || KIND == K_DOWN) {
+      // residual += acc: thread e -> row e >> 3, columns 2 (e & 7) .. +1 (4-byte sc1 access)
+      if (e < p.M * 8) {
+        const int m = e >> 3, n = 2 * (e & 7);
+        const auto rx = dev_rsrc(p.x);
+        const uint32_t off = static_cast<uint32_t>((static_cast<int64_t>(m) * p.H + tile * 16 + n) * 2);
+        const uint32_t old = __builtin_amdgcn_raw_buffer_load_b32(rx, off, 0, kScDevice);
+        const float v0 = bf(tobf(red_sum(m, n))) + bf(static_cast<uint16_t>(old & 0xffff));
+        const float v1 = bf(tobf(red_sum(m, n + 1))) + bf(static_cast<uint16_t>(old >> 16));
+        const uint32_t nv = static_cast<uint32_t>(tobf(v0)) | (static_cast<uint32_t>(tobf(v1)) << 16);
+        __builtin_amdgcn_raw_buffer_store_b32(nv, rx, off, 0, kScDevice);
+      }
+    } else if constexpr (KIND == K_GU) {
+      // silu(gate_j) * up_j for j = 2 (e & 3) .. +1 of row e >> 2 (tile covers act 8 t .. +7)
+      if (e < p.M * 4) {
+        const int m = e >> 2, j = 2 * (e & 3);
+        const float sc = inv_rms(m);
+        float o[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float g = bf(tobf(red_sum(m, j + h) * sc));
+          const float u = bf(tobf(red_sum(m, j + h + 8) * sc));
+          const float si = bf(tobf(g / (1.f + __expf(-g))));
+          o[h] = si * u;
+        }
+        const uint32_t nv = static_cast<uint32_t>(tobf(o[0])) | (static_cast<uint32_t>(tobf(o[1])) << 16);
+        const uint32_t off = static_cast<uint32_t>((static_cast<int64_t>(m) * p.I + tile * 8 + j) * 2);
+        __builtin_amdgcn_raw_buffer_store_b32(nv, dev_rsrc(p.act), off, 0, kScDevice);
+      }
+    } else if constexpr (KIND == K_QKV) {
+      // RoPE pairs (d, d + 64): tile = head * 8 + jj covers d = 8 jj .. +7 (cols 0-7) and
+      // d + 64 (cols 8-15); thread e -> row e >> 2, d pair 2 (e & 3) .. +1
+      if (e < p.M * 4) {
+        const int m = e >> 2, cc = 2 * (e & 3);
+        const int head = tile >> 3, d0 = (tile & 7) * 8 + cc;
+        const float sc = inv_rms(m);
+        const int nq = p.NQ, nkv = p.NKV;
+        const int slot = p.slots[m];
+        float o1[2], o2[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float x1 = bf(tobf(red_sum(m, cc + h) * sc));
+          const float x2 = bf(tobf(red_sum(m, cc + h + 8) * sc));
+          if (head < nq + nkv) {
+            const float* cs = p.cos_sin + static_cast<int64_t>(p.positions[m]) * 128;
+            const float co = cs[d0 + h], si = cs[64 + d0 + h];
+            o1[h] = x1 * co - x2 * si;
+            o2[h] = x2 * co + x1 * si;
+          } else {
+            o1[h] = x1;
+            o2[h] = x2;
+          }
+        }
+        const uint32_t lo = static_cast<uint32_t>(tobf(o1[0])) | (static_cast<uint32_t>(tobf(o1[1])) << 16);
+        const uint32_t hi = static_cast<uint32_t>(tobf(o2[0])) | (static_cast<uint32_t>(tobf(o2[1])) << 16);
+        const int BS = 1 << p.bs_shift;
+        if (head < nq) {
+          const auto rq = dev_rsrc(p.q);
+          const uint32_t off = static_cast<uint32_t>((static_cast<int64_t>(m) * nq * kD + head * kD + d0) * 2);
+          __builtin_amdgcn_raw_buffer_store_b32(lo, rq, off, 0, kScDevice);
+          __builtin_amdgcn_raw_buffer_store_b32(hi, rq, off + 128, 0, kScDevice);
+        } else if (slot >= 0 && head < nq + nkv) {
+          const int hk = head - nq;
+          uint16_t* kc = p.k_cache + layer * p.cache_layer_elems +
+                         ((static_cast<int64_t>(slot >> p.bs_shift) * nkv + hk) * BS + (slot & (BS - 1))) * kD;
+          // per-row cache addresses: device-scope (sc1) global stores, no per-thread rsrc
+          __hip_atomic_store(reinterpret_cast<uint32_t*>(kc + d0), lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(reinterpret_cast<uint32_t*>(kc + d0 + 64), hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (slot >= 0) {
+          const int hk = head - nq - nkv;
+          uint16_t* vc = p.v_cache + layer * p.cache_layer_elems +
+                         (static_cast<int64_t>(slot >> p.bs_shift) * nkv + hk) * kD * BS + (slot & (BS - 1));
+          __hip_atomic_store(vc + d0 * BS, static_cast<uint16_t>(lo & 0xffff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(vc + (d0 + 1) * BS, static_cast<uint16_t>(lo >> 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(vc + (d0 + 64) * BS, static_cast<uint16_t>(hi & 0xffff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(vc + (d0 + 65) * BS, static_cast<uint16_t>(hi >> 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    } else {  // LM head: Gumbel-max key of the tile's 16 vocab ids per row
+      if (e < p.M * 16) {
+        const int m = e >> 4, n = e & 15;
+        float v = bf(tobf(red_sum(m, n) * inv_rms(m)));
+        const float t = p.temperature[m];
+        const int idx = tile * 16 + n;
+        if (t > 1e-5f)
+          v = v / t + gumbel(static_cast<uint64_t>(p.seeds[m]), static_cast<uint64_t>(p.steps[m]),
+                             static_cast<uint32_t>(idx));
+        unsigned long long key = (static_cast<unsigned long long>(ordered_bits(v)) << 32) |
+                                 static_cast<unsigned long long>(0xFFFFFFFFu - static_cast<unsigned>(idx));
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          const unsigned long long other = __shfl_xor(key, o, kWave);
+          key = other > key ? other : key;
+        }
+        if (n == 0) {
+          const uint32_t off = static_cast<uint32_t>((static_cast<int64_t>(m) * (p.V / 16) + tile) * 8);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, key),
+                                                dev_rsrc(p.keys), off, 0, kScDevice);
+        }
+      }
+    }
+  }
+}
+
+// ---- attention phase ---------------------------------------------------------------------
+template <int G>
+__device__ void attention_phase(PP pp, Shared& sh_, int layer, unsigned* err) {
+  const auto& p = *fresh(pp);
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = lane & 15, grp = lane >> 4;
+  const int P = p.max_parts;
+  const int units = p.M * p.NKV * P;
+  const int BS = 1 << p.bs_shift;
+  const int64_t hs = static_cast<int64_t>(BS) * kD;
+  const uint16_t* kc_l = p.k_cache + layer * p.cache_layer_elems;
+  const uint16_t* vc_l = p.v_cache + layer * p.cache_layer_elems;
+  const auto rq = dev_rsrc(p.q);
+  const auto rpo = dev_rsrc(p.part_out);
+  const auto rpl = dev_rsrc(p.part_lse);
+  const auto ratt = dev_rsrc(p.attn);
+  constexpr float kNegInf = -__builtin_huge_valf();
+  for (int u = blockIdx.x; u < units; u += p.G) {
+    Shared& sh = fresh_lds(sh_);  // per-unit LDS addressing (no hoisted address registers)
+    const int s = u / (p.NKV * P);
+    const int hk = (u / P) % p.NKV;
+    const int part = u % P;
+    const int kvlen = p.seq_kvlen[s];
+    const int nparts = (kvlen + kPartTokens - 1) / kPartTokens;
+    if (part >= nparts) continue;  // workgroup-uniform
+    const int kv_begin = part * kPartTokens;
+    const int kv_end = min(kvlen, kv_begin + kPartTokens);
+    const int kt = kv_begin + w * 16;
+    const bool active = kt < kv_end;  // wave-uniform
+    // q fragment (col < G: head hk * G + col), 4 x 16 B
+    frag8 qf[4];
+    {
+      const bool ok = col < G;
+      const uint32_t off = static_cast<uint32_t>(
+          (static_cast<int64_t>(s) * p.NQ * kD + (hk * G + (ok ? col : 0)) * kD + 32 * grp) * 2);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+        qf[kk] = ok ? __builtin_bit_cast(frag8, dev_load16(rq, off + kk * 16)) : frag8{};
+    }
+    f32x4 o[8];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m_run = kNegInf, l_run = 0.f;
+    if (active) {
+      const int page = p.block_tables[static_cast<int64_t>(s) * p.bt_stride + (kt >> p.bs_shift)];
+      const auto rk = dev_rsrc(kc_l + (static_cast<int64_t>(page) * p.NKV + hk) * hs);
+      const auto rv = dev_rsrc(vc_l + (static_cast<int64_t>(page) * p.NKV + hk) * hs);
+      frag8 kf[4];
+      i16x4 vf[8];
+      const uint32_t koff = static_cast<uint32_t>((((kt + col) & (BS - 1)) * kD + 32 * grp) * 2);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) kf[kk] = __builtin_bit_cast(frag8, dev_load16(rk, koff + kk * 16));
+      const uint32_t voff = static_cast<uint32_t>((col * BS + ((kt + 4 * grp) & (BS - 1))) * 2);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+        vf[dt] = __builtin_bit_cast(i16x4, __builtin_amdgcn_raw_buffer_load_b64(rv, voff + dt * 16 * BS * 2, 0, kScDevice));
+      f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kk], qf[kk], sacc, 0, 0, 0);
+      float sv[4], tmax = kNegInf;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sv[j] = (kt + 4 * grp + j < kv_end) ? sacc[j] * p.scale_log2 : kNegInf;
+        tmax = fmaxf(tmax, sv[j]);
+      }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, kWave));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, kWave));
+      const float m_use = (tmax == kNegInf) ? 0.f : tmax;
+      float psum = 0.f;
+      i16x4 pf;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float pv = exp2f(sv[j] - m_use);
+        psum += pv;
+        pf[j] = static_cast<short>(tobf(pv));
+      }
+      psum += __shfl_xor(psum, 16, kWave);
+      psum += __shfl_xor(psum, 32, kWave);
+      l_run = psum;
+      m_run = tmax;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vf[dt], pf, o[dt], 0, 0, 0);
+    }
+    // ---- merge the 8 waves' states -------------------------------------------------------
+    AttS& as = sh.s.att;
+    if (col < G) {
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) as.o[w][col][16 * dt + 4 * grp + j] = o[dt][j];
+      if (grp == 0) {
+        as.m[w][col] = m_run;
+        as.l[w][col] = l_run;
+      }
+    }
+    cbar(sh, err);
+    const bool merger = threadIdx.x < G * 16;
+    const int cc = threadIdx.x >> 4;
+    const int d0 = (threadIdx.x & 15) * 8;
+    float r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float mu = 0.f, Lsum = 0.f;
+    if (merger) {
+      float mx = kNegInf;
+#pragma unroll
+      for (int q = 0; q < kCW; ++q) mx = fmaxf(mx, as.m[q][cc]);
+      mu = (mx == kNegInf) ? 0.f : mx;
+#pragma unroll
+      for (int q = 0; q < kCW; ++q) {
+        const float fw = exp2f(as.m[q][cc] - mu);
+        Lsum += fw * as.l[q][cc];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] += fw * as.o[q][cc][d0 + j];
+      }
+      const float invL = Lsum > 0.f ? 1.f / Lsum : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] *= invL;
+    }
+    const uint32_t out_off = static_cast<uint32_t>(
+        (static_cast<int64_t>(s) * p.NQ * kD + (hk * G + cc) * kD + d0) * 2);
+    if (nparts == 1) {
+      if (merger) {
+        u32x4 o8;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          o8[j] = static_cast<uint32_t>(tobf(r[2 * j])) | (static_cast<uint32_t>(tobf(r[2 * j + 1])) << 16);
+        dev_store16(ratt, out_off, o8);
+      }
+      cbar(sh, err);  // the scratch is reused by the next unit
+      continue;
+    }
+    const int64_t shk = static_cast<int64_t>(s) * p.NKV + hk;
+    if (merger) {
+      const int64_t base = (shk * P + part) * 16 + cc;
+      const uint32_t off = static_cast<uint32_t>((base * kD + d0) * 4);
+      dev_store16(rpo, off, __builtin_bit_cast(u32x4, f32x4{r[0], r[1], r[2], r[3]}));
+      dev_store16(rpo, off + 16, __builtin_bit_cast(u32x4, f32x4{r[4], r[5], r[6], r[7]}));
+      if ((threadIdx.x & 15) == 0)
+        dev_store4(rpl, static_cast<uint32_t>(base * 4), (Lsum > 0.f) ? (mu + log2f(Lsum)) : kNegInf);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    cbar(sh, err);
+    if (threadIdx.x == 0) {
+      const int old = __hip_atomic_fetch_add(p.att_counters + shk, 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      sh.bcast = (old == nparts - 1);
+    }
+    cbar(sh, err);
+    const bool last = sh.bcast != 0;
+    if (!last) continue;
+    // ---- last arriver: merge every partition (fixed order) ---------------------------------
+    {
+      constexpr int MG = G * 16;
+      constexpr int NG = kCW * 64 / MG < 8 ? kCW * 64 / MG : 8;
+      MergeS& ms = sh.s.mrg;
+      const int gidx = threadIdx.x / MG;
+      const int lt = threadIdx.x % MG;
+      const int mc = lt >> 4;
+      const int md0 = (lt & 15) * 8;
+      float mr = kNegInf, wsum = 0.f;
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (gidx < NG) {
+        for (int q = gidx; q < nparts; q += NG) {
+          const int64_t base = (shk * P + q) * 16 + mc;
+          const uint32_t off = static_cast<uint32_t>((base * kD + md0) * 4);
+          const float lse = dev_load4(rpl, static_cast<uint32_t>(base * 4));
+          const f32x4 pa = __builtin_bit_cast(f32x4, dev_load16(rpo, off));
+          const f32x4 pb = __builtin_bit_cast(f32x4, dev_load16(rpo, off + 16));
+          if (lse == kNegInf) continue;
+          const float m_new = fmaxf(mr, lse);
+          const float sc = exp2f(mr - m_new);
+          const float wt = exp2f(lse - m_new);
+          wsum = wsum * sc + wt;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            acc[jj] = acc[jj] * sc + wt * pa[jj];
+            acc[4 + jj] = acc[4 + jj] * sc + wt * pb[jj];
+          }
+          mr = m_new;
+        }
+      }
+      cbar(sh, err);  // as.* (aliased by ms) fully consumed by every merger thread above
+      if (gidx < NG) {
+        ms.mg[gidx][0][lt] = mr;
+        ms.mg[gidx][1][lt] = wsum;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) ms.mg[gidx][2 + jj][lt] = acc[jj];
+      }
+      cbar(sh, err);
+      if (gidx == 0) {
+        for (int g = 1; g < NG; ++g) {
+          const float gm = ms.mg[g][0][lt];
+          if (gm == kNegInf) continue;
+          const float m_new = fmaxf(mr, gm);
+          const float sc = exp2f(mr - m_new);
+          const float wt = exp2f(gm - m_new);
+          wsum = wsum * sc + wt * ms.mg[g][1][lt];
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) acc[jj] = acc[jj] * sc + wt * ms.mg[g][2 + jj][lt];
+          mr = m_new;
+        }
+        const float inv = wsum > 0.f ? 1.f / wsum : 0.f;
+        u32x4 o8;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          o8[j] = static_cast<uint32_t>(tobf(acc[2 * j] * inv)) |
+                  (static_cast<uint32_t>(tobf(acc[2 * j + 1] * inv)) << 16);
+        dev_store16(ratt, static_cast<uint32_t>(
+                              (static_cast<int64_t>(s) * p.NQ * kD + (hk * G + mc) * kD + md0) * 2),
+                    o8);
+      }
+      if (threadIdx.x == 0)
+        __hip_atomic_store(p.att_counters + shk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      cbar(sh, err);
+    }
+  }
+}
+
+// ---- the kernel ------------------------------------------------------------------------------
+template <int G>
+__global__ void __launch_bounds__(kThreads, 1) decode_step_kernel(const Params* __restrict__ gp) {
+  // the parameter block lives in device memory (a by-value aggregate whose address is taken
+  // is copied to scratch); each phase re-reads it through fresh()
+  __shared__ Shared sh;
+  const PP pp = (PP)gp;
+  const auto& p = *fresh(pp);
+  const int L = p.L;
+  const int NP = 3 + 5 * L;
+  unsigned* err = err_word(p, NP);
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x < kSlots) {
+    sh.full[threadIdx.x] = 0;
+    sh.freed[threadIdx.x] = 0;
+  }
+  if (threadIdx.x == 0) {
+    sh.bar_count = 0;
+    sh.bar_gen = 0;
+  }
+  __syncthreads();  // the only s_barrier: before the roles split
+  if (wave == kCW) {
+    loader(pp, sh, err);
+    return;
+  }
+  // row ids (token of each row: the previous step's device sample under look-ahead)
+  const int row = lane & 15;
+  const bool fp = p.feed_prev != nullptr && p.feed_prev[0] != 0;
+  int64_t id = 0;
+  if (row < p.M) id = fp ? p.prev_tokens[row] : static_cast<int64_t>(p.input_ids[row]);
+  // ---- E0: residual rows = embedding rows (workgroup m < M copies row m) ---------------------
+  if (static_cast<int>(blockIdx.x) < p.M) {
+    const int m = blockIdx.x;
+    const int64_t idm = fp ? p.prev_tokens[m] : static_cast<int64_t>(p.input_ids[m]);
+    const auto rx = dev_rsrc(p.x);
+    for (int k = threadIdx.x * 8; k < p.H; k += kCW * 64 * 8) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(p.embed + idm * p.H + k);
+      dev_store16(rx, static_cast<uint32_t>((static_cast<int64_t>(m) * p.H + k) * 2), v);
+    }
+  }
+  uint32_t seq = wave;  // this wave's chunk sequence: wave, wave + 8, ...
+  XSrc xres{dev_rsrc(p.x), p.H, false, nullptr};
+  for (int l = 0; l < L; ++l) {
+    const int base = 1 + 5 * l;
+    // QKV(l): layer 0 reads the embedding rows directly (no dependency); later layers wait
+    // for the previous layer's down projection
+    if (l > 0) {
+      if (wave == 0) poll_phase(p, base - 1, err);
+      cbar(sh, err);
+      if (wave == 0 && (base % p.G) == static_cast<int>(blockIdx.x) && base - 2 >= 1) zero_phase(p, base - 2);
+    }
+    if (l == 0) {
+      XSrc xe{dev_rsrc(p.x), p.H, true, p.embed + id * p.H};
+      gemv_phase<K_QKV>(pp, sh, l, xe, seq, err);
+    } else {
+      gemv_phase<K_QKV>(pp, sh, l, xres, seq, err);
+    }
+    arrive_phase(p, sh, base + K_QKV, err);
+    // ATT(l)
+    if (wave == 0) poll_phase(p, base + K_QKV, err);
+    cbar(sh, err);
+    if (wave == 0 && ((base + 1) % p.G) == static_cast<int>(blockIdx.x) && base - 1 >= 1) zero_phase(p, base - 1);
+    attention_phase<G>(pp, sh, l, err);
+    arrive_phase(p, sh, base + K_ATT, err);
+    // O(l)
+    if (wave == 0) poll_phase(p, base + K_ATT, err);
+    cbar(sh, err);
+    if (wave == 0 && ((base + 2) % p.G) == static_cast<int>(blockIdx.x)) zero_phase(p, base);
+    {
+      XSrc xa{dev_rsrc(p.attn), static_cast<int64_t>(p.NQ) * kD, false, nullptr};
+      gemv_phase<K_O>(pp, sh, l, xa, seq, err);
+    }
+    arrive_phase(p, sh, base + K_O, err);
+    // GU(l)
+    if (wave == 0) poll_phase(p, base + K_O, err);
+    cbar(sh, err);
+    if (wave == 0 && ((base + 3) % p.G) == static_cast<int>(blockIdx.x)) zero_phase(p, base + 1);
+    gemv_phase<K_GU>(pp, sh, l, xres, seq, err);
+    arrive_phase(p, sh, base + K_GU, err);
+    // DOWN(l)
+    if (wave == 0) poll_phase(p, base + K_GU, err);
+    cbar(sh, err);
+    if (wave == 0 && ((base + 4) % p.G) == static_cast<int>(blockIdx.x)) zero_phase(p, base + 2);
+    {
+      XSrc xd{dev_rsrc(p.act), p.I, false, nullptr};
+      gemv_phase<K_DOWN>(pp, sh, l, xd, seq, err);
+    }
+    arrive_phase(p, sh, base + K_DOWN, err);
+  }
+  // LM head + sampler keys
+  const int lm = 1 + 5 * L;
+  if (wave == 0) poll_phase(p, lm - 1, err);
+  cbar(sh, err);
+  if (wave == 0 && (lm % p.G) == static_cast<int>(blockIdx.x)) zero_phase(p, lm - 2);
+  gemv_phase<5>(pp, sh, 0, xres, seq, err);
+  arrive_phase(p, sh, lm, err);
+  // FIN: workgroup m < M reduces row m's tile keys to its token
+  if (static_cast<int>(blockIdx.x) < p.M) {
+    if (wave == 0) poll_phase(p, lm, err);
+    cbar(sh, err);
+    const int m = blockIdx.x;
+    const int nt = p.V / 16;
+    const auto rk = dev_rsrc(p.keys);
+    unsigned long long best = 0ull;
+    for (int i = threadIdx.x; i < nt; i += kCW * 64) {
+      const unsigned long long k = __builtin_bit_cast(
+          unsigned long long,
+          __builtin_amdgcn_raw_buffer_load_b64(rk, static_cast<uint32_t>((static_cast<int64_t>(m) * nt + i) * 8), 0, kScDevice));
+      best = k > best ? k : best;
+    }
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const unsigned long long other = __shfl_xor(best, o, kWave);
+      best = other > best ? other : best;
+    }
+    unsigned long long* red = reinterpret_cast<unsigned long long*>(&sh.s);
+    if (lane == 0) red[wave] = best;
+    cbar(sh, err);
+    if (threadIdx.x == 0) {
+      for (int q = 1; q < kCW; ++q) best = red[q] > best ? red[q] : best;
+      p.tokens[m] = static_cast<int64_t>(0xFFFFFFFFu - static_cast<unsigned>(best & 0xFFFFFFFFull));
+    }
+  }
+  // the last workgroup out re-zeroes the counters the in-flight zeroing could not reach
+  if (threadIdx.x == 0) {
+    unsigned* fw = final_word(p, NP);
+    const unsigned old = __hip_atomic_fetch_add(fw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == static_cast<unsigned>(p.G) - 1) {
+      for (int sh_ = 0; sh_ < kShards; ++sh_) {
+        __hip_atomic_store(ctr(p, lm - 1) + sh_ * kCtrStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ctr(p, lm) + sh_ * kCtrStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __hip_atomic_store(fw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Device copies of the parameter blocks, keyed by their bytes: one per (graph bucket,
+// metadata layout) - a handful per engine.  Built outside capture (the capture warm-up runs
+// the same call eagerly first); a miss while capturing returns nullptr.
+const Params* device_params(const Params& p, hipStream_t stream) {
+  static std::mutex mu;
+  static std::map<std::string, void*> cache;
+  const std::string key(reinterpret_cast<const char*>(&p), sizeof(Params));
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return static_cast<const Params*>(it->second);
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone)
+    return nullptr;
+  void* d = nullptr;
+  if (hipMalloc(&d, sizeof(Params)) != hipSuccess) return nullptr;
+  if (hipMemcpy(d, &p, sizeof(Params), hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+  cache.emplace(key, d);
+  return static_cast<const Params*>(d);
+}
+
+}  // namespace mk
+}  // namespace atta
+
+using namespace atta;
+
+int64_t atta_decode_step_sync_words(int layers) {
+  return static_cast<int64_t>(3 + 5 * layers) * mk::kShards * mk::kCtrStride + 2 * mk::kCtrStride;
+}
+
+int64_t atta_decode_step_error_index(int layers) {
+  return static_cast<int64_t>(3 + 5 * layers) * mk::kShards * mk::kCtrStride + mk::kCtrStride;
+}
+
+int atta_decode_step_grid() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+  return cus;
+}
+
+int atta_decode_step(const DecodeStepArgs& a, hipStream_t stream) {
+  if (a.M < 1 || a.M > mk::kRows) return -1;
+  if (a.H % 2048 || a.I % 2048 || (a.NQ * 128) % 2048) return -1;
+  if (a.NQ % a.NKV) return -1;
+  const int G = a.NQ / a.NKV;
+  if (G != 1 && G != 2 && G != 4) return -1;
+  if (a.block_size != 16) return -1;  // a 16-token attention tile = one page
+  if (a.max_parts < 1 || a.max_parts > 64) return -1;
+  const int grid = atta_decode_step_grid();
+  if (grid <= 0) return -1;
+  mk::Params p{};
+  p.M = a.M;
+  p.H = a.H;
+  p.I = a.I;
+  p.V = a.V;
+  p.L = a.L;
+  p.NQ = a.NQ;
+  p.NKV = a.NKV;
+  p.G = grid;
+  p.bt_stride = a.bt_stride;
+  p.bs_shift = 4;
+  p.max_parts = a.max_parts;
+  p.eps = a.eps;
+  p.scale_log2 = a.scale * 1.4426950408889634f;
+  p.layers = static_cast<const mk::LayerW*>(a.layers);
+  p.lm_head = static_cast<const uint16_t*>(a.lm_head);
+  p.embed = static_cast<const uint16_t*>(a.embed);
+  p.k_cache = static_cast<uint16_t*>(a.k_cache);
+  p.v_cache = static_cast<uint16_t*>(a.v_cache);
+  p.cache_layer_elems = a.cache_layer_elems;
+  p.input_ids = a.input_ids;
+  p.prev_tokens = a.prev_tokens;
+  p.feed_prev = a.feed_prev;
+  p.positions = a.positions;
+  p.slots = a.slots;
+  p.block_tables = a.block_tables;
+  p.seq_kvlen = a.seq_kvlen;
+  p.cos_sin = a.cos_sin;
+  p.temperature = a.temperature;
+  p.seeds = a.seeds;
+  p.steps = a.steps;
+  p.x = static_cast<uint16_t*>(a.x);
+  p.q = static_cast<uint16_t*>(a.q);
+  p.attn = static_cast<uint16_t*>(a.attn);
+  p.act = static_cast<uint16_t*>(a.act);
+  p.part_out = a.part_out;
+  p.part_lse = a.part_lse;
+  p.att_counters = a.att_counters;
+  p.keys = a.keys;
+  p.tokens = a.tokens;
+  p.sync = a.sync;
+  const mk::Params* dp = mk::device_params(p, stream);
+  if (dp == nullptr) return -3;  // first use of this parameter block while capturing
+  switch (G) {
+    case 1: mk::decode_step_kernel<1><<<grid, mk::kThreads, 0, stream>>>(dp); break;
+    case 2: mk::decode_step_kernel<2><<<grid, mk::kThreads, 0, stream>>>(dp); break;
+    default: mk::decode_step_kernel<4><<<grid, mk::kThreads, 0, stream>>>(dp); break;
+  }
+  return static_cast<int>(hipGetLastError());
+}

@@ -128,3 +128,40 @@ int64_t atta_ar2_error_offset();
 int atta_ar2_run(void* const* bases, int rank, int world, int64_t max_elems, const void* x,
                  void* y, const void* res, int64_t n, int dtype, hipStream_t stream);
 
+
+// ---- persistent decode step (decode_step.hip) --------------------------------------------
+struct DecodeStepArgs {
+  int M, H, I, V, L, NQ, NKV, bt_stride, max_parts, block_size;
+  float eps, scale;
+  const void* layers;  // device array [L] of {qkv, o, gate_up, down} pre-shuffled weight pointers
+  const void* lm_head;
+  const void* embed;
+  void* k_cache;
+  void* v_cache;
+  int64_t cache_layer_elems;
+  const int* input_ids;
+  const int64_t* prev_tokens;
+  const int* feed_prev;
+  const int* positions;
+  const int* slots;
+  const int* block_tables;
+  const int* seq_kvlen;
+  const float* cos_sin;
+  const float* temperature;
+  const int64_t* seeds;
+  const int64_t* steps;
+  void* x;
+  void* q;
+  void* attn;
+  void* act;
+  float* part_out;
+  float* part_lse;
+  int* att_counters;
+  unsigned long long* keys;
+  int64_t* tokens;
+  unsigned* sync;
+};
+int atta_decode_step(const DecodeStepArgs& a, hipStream_t stream);
+int64_t atta_decode_step_sync_words(int layers);
+int64_t atta_decode_step_error_index(int layers);
+int atta_decode_step_grid();
