@@ -379,6 +379,7 @@ class AgentAHandler(JsonHandler):
                         sp.set_attribute("app.agent_role", role)
                     headers = tracing.inject({"x-agent-index": str(idx)})
                     headers["X-Task-ID"] = run.task_id
+                    headers["x-fanout"] = str(len(workers))  # burst-aware LLM admission
                     return client.call_agent_b(sub, scenario=run.scenario, headers=headers,
                                                agent_b_role=role,
                                                agent_b_contract=w["contract"] or r["b_contract"],

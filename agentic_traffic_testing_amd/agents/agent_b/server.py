@@ -104,6 +104,11 @@ class AgentBHandler(JsonHandler):
                 if req_id:
                     headers["X-Request-ID"] = req_id
                 headers["X-Task-ID"] = task_id
+                # fan-out membership for the backend's burst-aware admission
+                if hdr.get("x-fanout"):
+                    headers["x-fanout"] = hdr.get("x-fanout")
+                    if agent_index:
+                        headers["x-agent-index"] = agent_index
                 try:
                     output, meta = client.call_llm(prompt, headers=headers, url=llm_url)
                 except Exception as exc:

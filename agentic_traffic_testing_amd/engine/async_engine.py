@@ -6,6 +6,15 @@ one output per engine step; llm/serve_llm.py:527-580).  Requests are handed to t
 engine thread through a lock-free deque so the event loop never blocks on a running GPU
 step; outputs come back with ``loop.call_soon_threadsafe``.
 
+Burst-aware admission: an agent fan-out reaches the backend as N requests
+a few ms apart (Agent A's ThreadPoolExecutor, reference agents/agent_a/server.py:534-623);
+admitted one by one, the first one's prefill runs alone and the rest queue behind it.  A
+request that carries its burst (``burst=(key, size)``: the X-Task-ID and the fan-out width
+Agent B forwards as ``x-fanout``) is held until its siblings are in or ``burst_window_s``
+has passed since the burst's first arrival, then the whole group is admitted together and
+shares ONE prefill forward.  Requests without burst information are never delayed.  TTFT
+still runs from each request's arrival, hold time included.
+
 Watchdog (SURVEY §5.3): ``heartbeat`` is refreshed every loop iteration;
 ``stalled(threshold)`` is true when work is pending but the loop has not progressed for
 ``threshold`` seconds, and the HTTP layer reports that on /health as 503.
@@ -27,8 +36,15 @@ class EngineDeadError(RuntimeError):
 
 
 class AsyncEngine:
-    def __init__(self, engine: LLMEngine, on_step=None, stream_interval_s: float = 0.05):
+    def __init__(self, engine: LLMEngine, on_step=None, stream_interval_s: float = 0.05,
+                 burst_window_s: float | None = None):
         self.engine = engine
+        if burst_window_s is None:
+            burst_window_s = getattr(engine.cfg, "burst_window_ms", 0.0) / 1000.0
+        self.burst_window_s = max(0.0, float(burst_window_s))
+        # held bursts: key -> [deadline, expected size, [pending entries in arrival order]]
+        self._held: dict[str, list] = {}
+        self.bursts_coalesced = 0  # groups admitted together (complete or at the deadline)
         self.on_step = on_step
         # intermediate outputs of a request are coalesced to at most one per interval (the
         # first token and the final output always go out at once): every delivery wakes the
@@ -61,7 +77,7 @@ class AsyncEngine:
         self.engine.shutdown()
 
     def stalled(self, threshold_s: float = 60.0) -> bool:
-        busy = bool(self._pending) or self.engine.has_unfinished()
+        busy = bool(self._pending) or bool(self._held) or self.engine.has_unfinished()
         return busy and (time.monotonic() - self.heartbeat) > threshold_s
 
     @property
@@ -69,15 +85,18 @@ class AsyncEngine:
         return self._thread is not None and self._thread.is_alive()
 
     # ------------------------------------------------------------------------------------
-    async def generate(self, prompt_ids, sampling: SamplingParams, request_id: str):
+    async def generate(self, prompt_ids, sampling: SamplingParams, request_id: str,
+                       burst: tuple | None = None):
         """Async generator of cumulative RequestOutputs: the first token at once, then at most
-        one per ``stream_interval_s``, and always the final one."""
+        one per ``stream_interval_s``, and always the final one.  ``burst``: (key, size) of
+        the fan-out this request belongs to (burst-aware admission, see the module doc)."""
         if not self.alive:
             raise EngineDeadError("engine loop is not running")
         loop = asyncio.get_running_loop()
         q: asyncio.Queue = asyncio.Queue()
         self._streams[request_id] = (loop, q)
-        self._pending.append((request_id, list(prompt_ids), sampling, time.perf_counter()))
+        self._pending.append((request_id, list(prompt_ids), sampling, time.perf_counter(),
+                              burst))
         self._wake.set()
         done = False
         try:
@@ -123,21 +142,60 @@ class AsyncEngine:
     def _fail_pending(self, err: BaseException):
         while self._pending:
             self._deliver(self._pending.popleft()[0], err)
+        for _, _, group in self._held.values():
+            for entry in group:
+                self._deliver(entry[0], err)
+        self._held.clear()
+
+    def _admit(self, entry):
+        rid, ids, sp, t_arr = entry[:4]
+        try:
+            self.engine.add_request(rid, ids, sp, arrival_time=t_arr)
+        except Exception as e:  # bad request: fail only that one
+            self._deliver(rid, e)
+
+    def _take_pending(self, now: float) -> float | None:
+        """Move arrived requests into the engine - bursts held until complete or expired.
+        Returns the earliest pending burst deadline (None: nothing held)."""
+        while self._pending:
+            entry = self._pending.popleft()
+            burst = entry[4] if len(entry) > 4 else None
+            if not burst or self.burst_window_s <= 0 or int(burst[1]) <= 1:
+                self._admit(entry)
+                continue
+            key, size = str(burst[0]), int(burst[1])
+            g = self._held.get(key)
+            if g is None:
+                g = self._held[key] = [entry[3] + self.burst_window_s, size, []]
+            g[2].append(entry)
+        nearest = None
+        for key in list(self._held):
+            deadline, size, group = self._held[key]
+            if len(group) >= size or now >= deadline:
+                del self._held[key]
+                for entry in group:  # arrival order: FIFO admission within the burst
+                    self._admit(entry)
+                self.bursts_coalesced += 1
+            elif nearest is None or deadline < nearest:
+                nearest = deadline
+        return nearest
 
     def _run(self):
         eng = self.engine
         while not self._stop.is_set():
             self.heartbeat = time.monotonic()
-            while self._pending:
-                rid, ids, sp, t_arr = self._pending.popleft()
-                try:
-                    eng.add_request(rid, ids, sp, arrival_time=t_arr)
-                except Exception as e:  # bad request: fail only that one
-                    self._deliver(rid, e)
+            nearest = self._take_pending(time.perf_counter())
             while self._aborts:
-                eng.abort(self._aborts.popleft())
+                rid = self._aborts.popleft()
+                for key in list(self._held):  # a held request that gave up
+                    g = self._held[key][2]
+                    g[:] = [e for e in g if e[0] != rid]
+                    if not g:
+                        del self._held[key]
+                eng.abort(rid)
             if not eng.has_unfinished():
-                self._wake.wait(0.05)
+                wait = 0.05 if nearest is None else max(0.0, nearest - time.perf_counter())
+                self._wake.wait(wait)
                 self._wake.clear()
                 continue
             try:

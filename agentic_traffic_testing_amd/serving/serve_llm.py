@@ -240,7 +240,17 @@ async def handle_chat(request: web.Request) -> web.Response:
             gen_span = None
             t_sub = time.monotonic()
             last_log = t_sub
-            async for out in st.aengine.generate(ids, sp, request_id):
+            # burst-aware admission: the fan-out width Agent A announces (x-fanout, forwarded
+            # by Agent B) groups the burst by its X-Task-ID
+            burst = None
+            fan = request.headers.get("x-fanout")
+            task = request.headers.get("X-Task-ID")
+            if fan and task:
+                try:
+                    burst = (task, int(fan))
+                except ValueError:
+                    burst = None
+            async for out in st.aengine.generate(ids, sp, request_id, burst=burst):
                 if gen_span is None:
                     queue_wait = time.monotonic() - t_sub
                     wait_span.set_attribute("llm_ttft_seconds", queue_wait)
