@@ -211,7 +211,7 @@ class EngineConfig:
     # burst-aware admission (engine/async_engine.py): requests that announce their fan-out
     # (X-Task-ID + x-fanout headers) are held up to this long for their siblings so the
     # burst shares one prefill; 0 disables.  Requests without the headers are never held.
-    burst_window_ms: float = 4.0
+    burst_window_ms: float = 10.0
     # async look-ahead decode: launch the next decode graph step before waiting for the
     # current one's tokens (llm_engine.LLMEngine.step)
     async_decode: bool = True

@@ -44,6 +44,9 @@ class AsyncEngine:
         self.burst_window_s = max(0.0, float(burst_window_s))
         # held bursts: key -> [deadline, expected size, [pending entries in arrival order]]
         self._held: dict[str, list] = {}
+        # bursts flushed at their deadline: key -> [stragglers still expected, expiry]; a
+        # late sibling is admitted at once instead of opening a new window
+        self._flushed: dict[str, list] = {}
         self.bursts_coalesced = 0  # groups admitted together (complete or at the deadline)
         self.on_step = on_step
         # intermediate outputs of a request are coalesced to at most one per interval (the
@@ -164,6 +167,13 @@ class AsyncEngine:
                 self._admit(entry)
                 continue
             key, size = str(burst[0]), int(burst[1])
+            late = self._flushed.get(key)
+            if late is not None:
+                late[0] -= 1
+                if late[0] <= 0 or now > late[1]:
+                    del self._flushed[key]
+                self._admit(entry)
+                continue
             g = self._held.get(key)
             if g is None:
                 g = self._held[key] = [entry[3] + self.burst_window_s, size, []]
@@ -173,6 +183,8 @@ class AsyncEngine:
             deadline, size, group = self._held[key]
             if len(group) >= size or now >= deadline:
                 del self._held[key]
+                if len(group) < size:
+                    self._flushed[key] = [size - len(group), now + 30.0]
                 for entry in group:  # arrival order: FIFO admission within the burst
                     self._admit(entry)
                 self.bursts_coalesced += 1

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import collections
 import json
 import os
 import random
@@ -59,6 +60,9 @@ class Settings:
         # benchmark knob: requests that do not say otherwise generate exactly max_tokens
         # (bench/e2e.py; random-init weights would otherwise stop at random EOS draws)
         self.ignore_eos = _env_bool("LLM_IGNORE_EOS", "")
+        # benchmark knob: clamp every request's max_tokens (0 = off) - e.g. the AgentVerse
+        # final synthesis asks for 4096 tokens, too long for a 70B stand-in run
+        self.max_tokens_limit = int(e.get("LLM_MAX_TOKENS_LIMIT") or "0")
         self.watchdog_s = float(e.get("LLM_WATCHDOG_SECONDS", "120"))
         # fault injection: exercise the agents' error / timeout paths
         self.fault_fail_rate = float(e.get("LLM_FAULT_FAIL_RATE") or "0")
@@ -77,6 +81,10 @@ class ServerState:
             LLMMetrics(self.s.metrics_prefix) if self.s.metrics_enabled else None)
         self.tracer = otel.get_tracer("llm-backend")
         self.inflight = 0
+        self.peak_inflight = 0
+        # per-request records of completed calls (bench/e2e.py reads them for workloads whose
+        # clients do not see the backend meta, e.g. the OpenAI proxy)
+        self.records: collections.deque = collections.deque(maxlen=200000)
         self.last_arrival: float | None = None
         self.model_name = model_name
         self.tok = engine.tokenizer if engine is not None else None
@@ -163,6 +171,7 @@ async def handle_chat(request: web.Request) -> web.Response:
             st.metrics.interarrival.observe(start - st.last_arrival)
         st.last_arrival = start
         st.inflight += 1
+        st.peak_inflight = max(st.peak_inflight, st.inflight)
         current_inflight = st.inflight
         if st.metrics:
             st.metrics.inflight.inc()
@@ -202,6 +211,8 @@ async def handle_chat(request: web.Request) -> web.Response:
             prompt = apply_chat_template(prompt, data.get("system_prompt"))
         ids = st.tok.encode(prompt)
         eff_new = max_tokens if max_tokens is not None else st.s.max_tokens
+        if st.s.max_tokens_limit > 0:
+            eff_new = min(eff_new, st.s.max_tokens_limit)
         truncated_tokens = None
         mml = st.s.max_model_len_env
         if mml > 0:
@@ -300,6 +311,9 @@ async def handle_chat(request: web.Request) -> web.Response:
         if st.s.log_requests:
             st.log(f"[llm-metrics] status=success latency_ms={latency_ms} prompt_tokens="
                    f"{prompt_tokens} completion_tokens={completion_tokens}")
+        st.records.append({"t_end": time.time(), "queue_wait_s": queue_wait,
+                           "prompt_tokens": prompt_tokens,
+                           "completion_tokens": completion_tokens, "burst": burst})
         meta = {
             "request_id": request_id,
             "latency_ms": latency_ms,

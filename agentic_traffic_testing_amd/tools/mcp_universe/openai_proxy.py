@@ -140,11 +140,7 @@ async def _serve(host: str, port: int, backend_url: str) -> None:
     runner = web.AppRunner(create_app(backend_url))
     await runner.setup()
     await web.TCPSite(runner, host, port).start()
-    print("=" * 60)
-    print("[*] OpenAI proxy for MCP-Universe ready")
-    print(f"    Listening on http://{host}:{port}")
-    print(f"    Forwarding to local LLM backend: {backend_url}")
-    print("=" * 60, flush=True)
+    print(f"[openai-proxy] listening on http://{host}:{port} -> {backend_url}", flush=True)
     try:
         while True:
             await asyncio.sleep(3600)
@@ -162,7 +158,7 @@ def main(argv: list[str] | None = None) -> None:
     try:
         asyncio.run(_serve(a.host, a.port, a.backend_url))
     except KeyboardInterrupt:
-        print("\n[*] OpenAI proxy shutting down.")
+        print("[openai-proxy] stopped", flush=True)
 
 
 if __name__ == "__main__":

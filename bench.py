@@ -90,6 +90,13 @@ def parse_args(argv=None):
     ap.add_argument("--tp-same-device", action="store_true",
                     help="--parallel tp rehearsal with every rank on cuda:0 (IPC collectives, "
                          "graph-captured decode): the TP protocol on a one-GPU box")
+    ap.add_argument("--workload", choices=["agentic_parallel", "agentverse", "proxy"],
+                    default="agentic_parallel",
+                    help="--via http workload: the /task fan-out (headline), the AgentVerse "
+                         "loop (POST /agentverse, config 4) or multi-turn agents through the "
+                         "OpenAI-compatible proxy (config 5's MCP-Universe path)")
+    ap.add_argument("--max-tokens-limit", type=int, default=0,
+                    help="--via http: clamp every LLM call's max_tokens (0 = off)")
     ap.add_argument("--via", choices=["engine", "http"], default="engine",
                     help="engine: drive the engine in-process (headline); http: the whole "
                          "serving stack - aiohttp llm-backend + Agent A + 5 Agent B over "
@@ -284,7 +291,8 @@ def _finish_http(a, eng, world, rank, dist, init_s, cfg, log):
     if dist:
         dist.barrier()
     _sync(a)
-    r = run_e2e(eng, a.steps, a.warmup, fanout=a.fanout, max_tokens=a.max_tokens, log=log)
+    r = run_e2e(eng, a.steps, a.warmup, fanout=a.fanout, max_tokens=a.max_tokens, log=log,
+                workload=a.workload, max_tokens_limit=a.max_tokens_limit)
     _sync(a)
     elapsed, tokens = r["seconds"], r["tokens"]
     per_rank = [round(r["tokens_per_s"], 2)]
@@ -306,7 +314,7 @@ def _finish_http(a, eng, world, rank, dist, init_s, cfg, log):
             "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16" if "bf" in a.dtype else a.dtype,
             "weights": a.quantization or ("bf16" if "bf" in a.dtype else a.dtype),
-            "data": DATA.format(label), "via": "http",
+            "data": DATA.format(label), "via": "http", "workload": a.workload,
             "config": {"model": f"{label} (random-init)", "global_batch": a.fanout * world,
                        "seq_len": a.max_model_len,
                        "parallelism": f"dp{world}" if world > 1 else "tp1",
@@ -316,7 +324,9 @@ def _finish_http(a, eng, world, rank, dist, init_s, cfg, log):
             "per_rank_tokens_per_s": per_rank,
             "p50_ttft_s": round(p50, 4) if p50 is not None else None,
             "p95_ttft_s": round(p95, 4) if p95 is not None else None,
-            "llm_calls": r["calls"], "completion_tokens": int(tokens),
+            "llm_calls": r["calls"], "llm_calls_per_workflow": r["calls_per_workflow"],
+            "peak_inflight": r["peak_inflight"], "bursts_coalesced": r["bursts_coalesced"],
+            "completion_tokens": int(tokens),
             "per_task_s": r["per_task_s"], "init_s": round(init_s, 1)}), flush=True)
     if dist:
         dist.barrier()

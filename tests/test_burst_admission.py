@@ -69,3 +69,10 @@ def test_burst_window_zero_disables_holding():
     plan = [(0.0, "d0", ("task-4", 5))]
     steps, ttft, ae = _run(0.0, plan)
     assert ttft["d0"] < 0.5
+
+
+def test_straggler_after_deadline_not_held_again():
+    """A sibling arriving after its burst was flushed at the deadline is admitted at once."""
+    plan = [(0.0, "e0", ("task-5", 2)), (0.3, "e1", ("task-5", 2))]
+    steps, ttft, ae = _run(0.05, plan)
+    assert ttft["e1"] < 0.04, ttft  # no second 50 ms window
