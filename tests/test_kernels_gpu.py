@@ -690,3 +690,50 @@ def test_stream_read_probe(nbytes):
     ops._native().stream_read(x, sink)
     torch.cuda.synchronize()
     assert bool((sink == 0).all())
+
+
+@pytest.mark.parametrize("m", [1, 5, 16])
+def test_fp8_decode_kernels_vs_fp32_reference(m):
+    """the fp8 weight-only decode GEMVs against the fp32 PyTorch reference
+    (ops/reference.py) of the same op on the dequantised weights - not against another
+    kernel.  Plain projection, residual add, fused RMSNorm + gate_up + SiLU*up, fused
+    RMSNorm + QKV + RoPE + paged K/V write."""
+    torch.manual_seed(41)
+    dt, H = torch.bfloat16, 2048
+    x = torch.randn(m, H, dtype=dt, device="cuda")
+    xf = x.float()
+
+    def q(w, rowmap="plain"):
+        qw, sc = ops.quantize_fp8(w)
+        return ops.preshuffle_fp8(qw, rowmap), sc, ops.dequantize_fp8(qw, sc, torch.float32)
+
+    w = torch.randn(1024, H, dtype=dt, device="cuda") * 0.05
+    wq, sc, wf = q(w)
+    exp = xf @ wf.t()
+    close(ops.linear(x, wq, w_scale=sc), exp, 2e-2, 1e-2)
+    res = torch.randn(m, 1024, dtype=dt, device="cuda")
+    want = res.float() + exp
+    ops.linear(x, wq, residual=res, w_scale=sc)
+    close(res, want, 4e-2, 1e-2)
+    eps, inter = 1e-5, 512
+    ones = torch.ones(H, dtype=torch.float32, device="cuda")
+    wg = torch.randn(2 * inter, H, dtype=dt, device="cuda") * 0.05
+    gq, gs, gf = q(wg, "silu")
+    exp = ref.silu_and_mul(ref.rms_norm(xf, ones, eps) @ gf.t())
+    close(ops.decode_gate_up_silu(x, gq, eps, w_scale=gs), exp, 3e-2, 3e-2)
+    hq, hkv, bs, nb = 8, 2, 16, 8
+    wqkv = torch.randn((hq + 2 * hkv) * 128, H, dtype=dt, device="cuda") * 0.05
+    kq, ks, kf = q(wqkv, "qkv")
+    kc = torch.zeros(nb, hkv, bs, 128, dtype=dt, device="cuda")
+    vc = torch.zeros(nb, hkv, 128, bs, dtype=dt, device="cuda")
+    kc_r = torch.zeros(nb, hkv, bs, 128, dtype=torch.float32, device="cuda")
+    vc_r = torch.zeros(nb, hkv, 128, bs, dtype=torch.float32, device="cuda")
+    pos = torch.arange(3, 3 + m, dtype=torch.int32, device="cuda")
+    slots = torch.arange(m, dtype=torch.int32, device="cuda") * 3
+    cs = ref.rope_cos_sin(128, 64, 500000.0, None, device="cuda")
+    got = ops.decode_qkv_rope(x, kq, eps, pos, slots, cs, kc, vc, hq, hkv, w_scale=ks)
+    qkv = ref.rms_norm(xf, ones, eps) @ kf.t()
+    exp = ref.rope_cache(qkv, pos, slots, cs, kc_r, vc_r, hq, hkv, 128)
+    close(got, exp, 3e-2, 3e-2)
+    close(kc, kc_r, 3e-2, 3e-2)
+    close(vc, vc_r, 3e-2, 3e-2)

@@ -26,4 +26,22 @@ const U = {
   hostOf(url) { try { return new URL(url).host; } catch (e) { return String(url || ''); } },
   baseOf(endpoint) { return String(endpoint).replace(/\/agentverse\/?$/, ''); },
   queryParam(name) { return new URLSearchParams(location.search).get(name); },
+  // clipboard with a fallback for plain-http pages (navigator.clipboard needs a secure context)
+  copy(text) {
+    text = String(U.nz(text, ''));
+    if (typeof navigator !== 'undefined' && navigator.clipboard && window.isSecureContext) {
+      return navigator.clipboard.writeText(text);
+    }
+    return new Promise((resolve, reject) => {
+      const ta = U.el('textarea', { style: 'position:fixed;left:-9999px' });
+      ta.value = text;
+      document.body.appendChild(ta);
+      ta.select();
+      const ok = document.execCommand('copy');
+      ta.remove();
+      if (ok) resolve(); else reject(new Error('copy failed'));
+    });
+  },
 };
+
+if (typeof module !== 'undefined') module.exports = { U };
