@@ -630,10 +630,10 @@ class ModelRunner:
             for _ in range(2):  # warm up (hipBLASLt heuristics, allocator)
                 self._forward_sample(v, md, parts, special)
         torch.cuda.current_stream(self.device).wait_stream(stream)
-        g = torch.cuda.CUDAGraph()
         dump_dir = os.environ.get("ATTA_GRAPH_DUMP_DIR")
-        if dump_dir:  # node-level dump of every captured step (scripts/gpu/graph_nodes.py)
-            g.enable_debug_mode()
+        # node-level dump of every captured step (scripts/gpu/graph_nodes.py) keeps the
+        # hipGraph after instantiation so its nodes can be listed
+        g = torch.cuda.CUDAGraph(keep_graph=True) if dump_dir else torch.cuda.CUDAGraph()
         if self.graph_pool is None:
             self.graph_pool = torch.cuda.graph_pool_handle()
         with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
@@ -647,8 +647,11 @@ class ModelRunner:
         key = (bucket, parts, int(special))
         if dump_dir:
             os.makedirs(dump_dir, exist_ok=True)
-            g.debug_dump(os.path.join(
-                dump_dir, f"tp{self.tp_size}_rank{self.tp_rank}_b{bucket}_p{parts}_s{int(special)}.dot"))
+            nodes = ops._native().graph_nodes(int(g.raw_cuda_graph()))
+            path = os.path.join(dump_dir, f"tp{self.tp_size}_rank{self.tp_rank}_b{bucket}"
+                                          f"_p{parts}_s{int(special)}.nodes")
+            with open(path, "w") as f:
+                f.write("\n".join(nodes) + "\n")
         self.graphs[key] = g
         self.graph_io[key] = {"layout": lay, "dev": dev, "out": out}
 

@@ -649,6 +649,18 @@ def decode_step_error(sync: torch.Tensor, layers: int) -> int:
     return int(sync[int(_native().decode_step_error_index(layers))].item())
 
 
+def set_decode_step_trace(trace: torch.Tensor | None = None, stats: torch.Tensor | None = None):
+    """Profiling of the persistent decode-step launches that follow (None: off): ``trace``
+    int64 [grid, 3 + 5 L, 2] wall-clock stamps (100 MHz) of every phase's begin (after its
+    poll) and end (before its arrival) per workgroup; ``stats`` int64 [grid, 4] shader cycles
+    of loader FREE waits, loader lifetime, wave-0 FULL waits and wave-0 poll waits."""
+    _native().set_decode_step_trace(trace, stats)
+
+
+def decode_step_grid() -> int:
+    return int(_native().decode_step_grid())
+
+
 def decode_step(layers_table: torch.Tensor, lm_head: torch.Tensor, embed: torch.Tensor,
                 k_cache: torch.Tensor, v_cache: torch.Tensor, md, input_ids: torch.Tensor,
                 prev_tokens: torch.Tensor, feed_prev: torch.Tensor, cos_sin: torch.Tensor,

@@ -5,6 +5,8 @@
 // allocation, no sync).  Ops only accept device tensors: CPU execution of the same math
 // lives in ops/reference.py and is selected by the Python wrappers by tensor device,
 // never as a silent fallback for a GPU tensor.
+#include <string>
+#include <vector>
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
@@ -673,6 +675,55 @@ int64_t decode_step_error_index(int64_t layers) {
 }
 int64_t decode_step_grid() { return atta_decode_step_grid(); }
 
+// Node list of a captured hipGraph (torch.cuda.CUDAGraph(keep_graph=True).raw_cuda_graph()):
+// "kernel:<name> grid=x,y,z block=x" / "memcpy" / "memset" / "host" / ... in graph order -
+// evidence of what a captured decode step contains (scripts/gpu/graph_nodes.py).
+std::vector<std::string> graph_nodes(int64_t graph) {
+  auto g = reinterpret_cast<hipGraph_t>(graph);
+  size_t n = 0;
+  check_rc(static_cast<int>(hipGraphGetNodes(g, nullptr, &n)), "hipGraphGetNodes");
+  std::vector<hipGraphNode_t> nodes(n);
+  check_rc(static_cast<int>(hipGraphGetNodes(g, nodes.data(), &n)), "hipGraphGetNodes");
+  std::vector<std::string> out;
+  for (auto node : nodes) {
+    hipGraphNodeType t;
+    check_rc(static_cast<int>(hipGraphNodeGetType(node, &t)), "hipGraphNodeGetType");
+    switch (t) {
+      case hipGraphNodeTypeKernel: {
+        hipKernelNodeParams kp{};
+        std::string name = "?";
+        if (hipGraphKernelNodeGetParams(node, &kp) == hipSuccess && kp.func != nullptr) {
+          const char* nm = hipKernelNameRefByPtr(kp.func, nullptr);
+          if (nm == nullptr) nm = hipKernelNameRef(reinterpret_cast<hipFunction_t>(kp.func));
+          if (nm != nullptr) name = nm;
+        }
+        out.push_back("kernel:" + name + " grid=" + std::to_string(kp.gridDim.x) + "," +
+                      std::to_string(kp.gridDim.y) + "," + std::to_string(kp.gridDim.z) +
+                      " block=" + std::to_string(kp.blockDim.x));
+        break;
+      }
+      case hipGraphNodeTypeMemcpy: out.push_back("memcpy"); break;
+      case hipGraphNodeTypeMemset: out.push_back("memset"); break;
+      case hipGraphNodeTypeHost: out.push_back("host"); break;
+      case hipGraphNodeTypeEmpty: out.push_back("empty"); break;
+      case hipGraphNodeTypeWaitEvent: out.push_back("wait_event"); break;
+      case hipGraphNodeTypeEventRecord: out.push_back("event_record"); break;
+      default: out.push_back("other:" + std::to_string(static_cast<int>(t))); break;
+    }
+  }
+  return out;
+}
+
+void set_decode_step_trace(const c10::optional<at::Tensor>& trace,
+                           const c10::optional<at::Tensor>& stats) {
+  for (const auto* t : {&trace, &stats})
+    if (t->has_value())
+      TORCH_CHECK((*t)->is_cuda() && (*t)->scalar_type() == at::kLong && (*t)->is_contiguous(),
+                  "set_decode_step_trace: int64 cuda tensors");
+  atta_set_decode_step_trace(trace.has_value() ? trace->data_ptr() : nullptr,
+                             stats.has_value() ? stats->data_ptr() : nullptr);
+}
+
 }  // namespace
 
 TORCH_LIBRARY(atta, m) {
@@ -680,6 +731,8 @@ TORCH_LIBRARY(atta, m) {
   m.def("decode_step_sync_words(int layers) -> int", &decode_step_sync_words);
   m.def("decode_step_error_index(int layers) -> int", &decode_step_error_index);
   m.def("decode_step_grid() -> int", &decode_step_grid);
+  m.def("set_decode_step_trace(Tensor? trace, Tensor? stats) -> ()", &set_decode_step_trace);
+  m.def("graph_nodes(int graph) -> str[]", &graph_nodes);
   m.def("ar_buffer_bytes(int max_elems, int elem_bytes) -> int", &ar_buffer_bytes);
   m.def("ar_alloc(int bytes, int device) -> int", &ar_alloc);
   m.def("set_attention_trace(Tensor? trace) -> ()", &set_attention_trace);

@@ -20,8 +20,8 @@
 //   * ring: 16 slots of 8 KiB, slot = seq & 15 for the workgroup's chunk sequence; chunk
 //     seq is consumed by wave seq & 7, so each wave owns two alternating slots.  FULL /
 //     FREE generation words in LDS: the loader publishes a slot behind a counted vmcnt that
-//     keeps the next two chunks in flight; a wave releases a slot as soon as its 8 KiB are
-//     in registers (before the MFMAs).
+//     keeps the next kInFlight chunks in flight; a wave releases a slot as soon as its 8 KiB
+//     are in registers (before the MFMAs).
 //   * activations (x) are read by the compute waves straight from global memory with
 //     device-scope (sc1) buffer loads, one chunk ahead; the norm's sum of squares comes from
 //     the same fragments.  Waves combine their K-slice partials through LDS; epilogues
@@ -64,6 +64,10 @@ constexpr int kCtrStride = 16;            // uint32 words between counter shards
 constexpr int kMaxG = 4;                  // GQA group
 constexpr int kPartTokens = kCW * 16;     // attention partition = 8 waves x 16 tokens
 constexpr unsigned kSpinLimit = 1u << 24;
+// chunks the loader keeps in flight before publishing one (vmcnt counts 1 KiB DMAs): 2 chunks
+// = 16 KiB per CU in flight measured 6.3 ms per 8B decode step (~2.4 TB/s: latency-bound)
+constexpr int kInFlight = 6;
+static_assert(8 * kInFlight <= 63, "vmcnt field");
 
 // error word bits
 constexpr unsigned kErrPoll = 1u, kErrFull = 2u, kErrFree = 4u, kErrBar = 8u;
@@ -106,6 +110,11 @@ struct Params {
   unsigned long long* keys;  // [M, V / 16]
   int64_t* tokens;
   unsigned* sync;  // [NP][kShards][kCtrStride] counters, final counter, error word
+  // optional profiling (ops.set_decode_step_trace): per workgroup [NP][2] wall-clock stamps
+  // (phase begin after its poll, phase end before its arrival) and 4 shader-cycle counters
+  // (loader FREE waits, loader total, wave-0 FULL waits, wave-0 poll waits)
+  unsigned long long* trace;
+  unsigned long long* stats;
 };
 
 enum Kind { K_QKV = 0, K_ATT = 1, K_O = 2, K_GU = 3, K_DOWN = 4 };
@@ -135,6 +144,7 @@ struct Shared {
   unsigned freed[kSlots];
   unsigned bar_count, bar_gen;
   int bcast;
+  unsigned long long full_wait, poll_wait;  // profiling (wave 0)
 };
 
 // Opaque copy of the parameter-block pointer: loads through it cannot be hoisted across the
@@ -201,6 +211,7 @@ __device__ __forceinline__ unsigned* final_word(const P& p, int np) {
 template <typename P>
 __device__ __forceinline__ void poll_phase(const P& p, int phase, unsigned* err) {
   const int lane = threadIdx.x & 63;
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   unsigned* c = ctr(p, phase);
   const unsigned want = lane < kShards ? static_cast<unsigned>((p.G - lane + kShards - 1) / kShards) : 0u;
   for (unsigned spins = 0;; ++spins) {
@@ -214,6 +225,10 @@ __device__ __forceinline__ void poll_phase(const P& p, int phase, unsigned* err)
     }
     __builtin_amdgcn_s_sleep(1);
   }
+  if (p.stats != nullptr && lane == 0)
+    p.stats[blockIdx.x * 4 + 3] += __builtin_amdgcn_s_memtime() - t0;
+  if (p.trace != nullptr && lane == 0)  // phase `phase + 1` begins
+    p.trace[(static_cast<int64_t>(blockIdx.x) * (3 + 5 * p.L) + phase + 1) * 2] = wall_clock64();
 }
 
 template <typename P>
@@ -230,6 +245,8 @@ __device__ __forceinline__ void arrive_phase(const P& p, Shared& sh, int phase,
                                              unsigned* err) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   cbar(sh, err);
+  if (p.trace != nullptr && threadIdx.x == 0)
+    p.trace[(static_cast<int64_t>(blockIdx.x) * (3 + 5 * p.L) + phase) * 2 + 1] = wall_clock64();
   if (threadIdx.x == 0)
     __hip_atomic_fetch_add(ctr(p, phase) + (blockIdx.x & (kShards - 1)) * kCtrStride, 1u,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -276,6 +293,8 @@ __device__ void loader(PP pp, Shared& sh, unsigned* err) {
   const uint32_t ring0 = __builtin_amdgcn_readfirstlane(
       static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sh.ring)));
   uint32_t seq = 0;
+  unsigned long long free_wait = 0;
+  const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
   auto publish = [&](uint32_t s) {
     __atomic_store_n(&sh.full[s & (kSlots - 1)], (s >> 4) + 1, __ATOMIC_RELAXED);
   };
@@ -292,7 +311,8 @@ __device__ void loader(PP pp, Shared& sh, unsigned* err) {
         for (int w = 0; w < kCW; ++w) {
           const int slot = seq & (kSlots - 1);
           const unsigned gen = (seq >> 4) + 1;
-          if (gen > 1) {
+          if (gen > 1 && ld_volatile(&sh.freed[slot]) + 1 < gen) {
+            const unsigned long long tw = __builtin_amdgcn_s_memtime();
             unsigned spins = 0;
             while (ld_volatile(&sh.freed[slot]) + 1 < gen) {
               __builtin_amdgcn_s_sleep(0);
@@ -301,15 +321,16 @@ __device__ void loader(PP pp, Shared& sh, unsigned* err) {
                 break;
               }
             }
+            free_wait += __builtin_amdgcn_s_memtime() - tw;
           }
           const uint16_t* src = tb + (static_cast<int64_t>(w * nb + j * 8) * 512) + lane * 8;
           const uint32_t dst = __builtin_amdgcn_readfirstlane(ring0 + slot * kSlotBytes);
 #pragma unroll
           for (int u = 0; u < 8; ++u)
             dma16(src + u * 512, __builtin_amdgcn_readfirstlane(dst + u * 1024));
-          if (seq >= 2) {
-            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-            publish(seq - 2);
+          if (seq >= kInFlight) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 * kInFlight) : "memory");
+            publish(seq - kInFlight);
           }
           ++seq;
         }
@@ -317,8 +338,11 @@ __device__ void loader(PP pp, Shared& sh, unsigned* err) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (seq >= 2) publish(seq - 2);
-  if (seq >= 1) publish(seq - 1);
+  for (uint32_t s = seq > kInFlight ? seq - kInFlight : 0; s < seq; ++s) publish(s);
+  if (p.stats != nullptr && lane == 0) {
+    p.stats[blockIdx.x * 4 + 0] = free_wait;
+    p.stats[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memtime() - t_begin;
+  }
 }
 
 // ---- compute-wave GEMV phase ----------------------------------------------------------------
@@ -400,7 +424,8 @@ __device__ void gemv_phase(PP pp, Shared& sh_, int layer, const XSrc& xs,
       load_x(xa, j);
       const int slot = seq & (kSlots - 1);
       const unsigned gen = (seq >> 4) + 1;
-      if (lane == 0) {
+      if (lane == 0 && ld_volatile(&sh.full[slot]) < gen) {
+        const unsigned long long tw = __builtin_amdgcn_s_memtime();
         unsigned spins = 0;
         while (ld_volatile(&sh.full[slot]) < gen) {
           __builtin_amdgcn_s_sleep(0);
@@ -409,6 +434,8 @@ __device__ void gemv_phase(PP pp, Shared& sh_, int layer, const XSrc& xs,
             break;
           }
         }
+        if (w == 0 && p.stats != nullptr)
+          sh.full_wait += __builtin_amdgcn_s_memtime() - tw;
       }
       __builtin_amdgcn_wave_barrier();
       const uint8_t* sb = sh.ring + slot * kSlotBytes + lane * 16;
@@ -794,6 +821,8 @@ __global__ void __launch_bounds__(kThreads, 1) decode_step_kernel(const Params* 
   if (threadIdx.x == 0) {
     sh.bar_count = 0;
     sh.bar_gen = 0;
+    sh.full_wait = 0;
+    if (p.stats != nullptr) p.stats[blockIdx.x * 4 + 3] = 0;
   }
   __syncthreads();  // the only s_barrier: before the roles split
   if (wave == kCW) {
@@ -898,6 +927,7 @@ __global__ void __launch_bounds__(kThreads, 1) decode_step_kernel(const Params* 
       p.tokens[m] = static_cast<int64_t>(0xFFFFFFFFu - static_cast<unsigned>(best & 0xFFFFFFFFull));
     }
   }
+  if (p.stats != nullptr && threadIdx.x == 0) p.stats[blockIdx.x * 4 + 2] = sh.full_wait;
   // the last workgroup out re-zeroes the counters the in-flight zeroing could not reach
   if (threadIdx.x == 0) {
     unsigned* fw = final_word(p, NP);
@@ -952,6 +982,14 @@ int atta_decode_step_grid() {
   return cus;
 }
 
+static unsigned long long* g_mk_trace = nullptr;
+static unsigned long long* g_mk_stats = nullptr;
+
+void atta_set_decode_step_trace(void* trace, void* stats) {
+  g_mk_trace = static_cast<unsigned long long*>(trace);
+  g_mk_stats = static_cast<unsigned long long*>(stats);
+}
+
 int atta_decode_step(const DecodeStepArgs& a, hipStream_t stream) {
   if (a.M < 1 || a.M > mk::kRows) return -1;
   if (a.H % 2048 || a.I % 2048 || (a.NQ * 128) % 2048) return -1;
@@ -1003,6 +1041,8 @@ int atta_decode_step(const DecodeStepArgs& a, hipStream_t stream) {
   p.keys = a.keys;
   p.tokens = a.tokens;
   p.sync = a.sync;
+  p.trace = g_mk_trace;
+  p.stats = g_mk_stats;
   const mk::Params* dp = mk::device_params(p, stream);
   if (dp == nullptr) return -3;  // first use of this parameter block while capturing
   switch (G) {

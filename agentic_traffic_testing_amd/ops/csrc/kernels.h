@@ -165,3 +165,5 @@ int atta_decode_step(const DecodeStepArgs& a, hipStream_t stream);
 int64_t atta_decode_step_sync_words(int layers);
 int64_t atta_decode_step_error_index(int layers);
 int atta_decode_step_grid();
+// profiling buffers of later persistent-step launches (nullptr: off): see decode_step.hip
+void atta_set_decode_step_trace(void* trace, void* stats);

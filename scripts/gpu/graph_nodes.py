@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Summarise the nodes of captured decode-step hipGraphs (``ATTA_GRAPH_DUMP_DIR`` dumps).
 
-``ModelRunner.capture`` writes one DOT file per captured (rank, bucket, partitions) graph when
-``ATTA_GRAPH_DUMP_DIR`` is set (torch.cuda.CUDAGraph.debug_dump).  This script lists, per
+``ModelRunner.capture`` writes one ``.nodes`` file per captured (rank, bucket, partitions)
+graph when ``ATTA_GRAPH_DUMP_DIR`` is set: the graph's node list read back with
+hipGraphGetNodes / hipGraphKernelNodeGetParams (ops graph_nodes binding).  This lists, per
 file, the node kinds (kernel / memcpy / memset / host / event ...) and the kernel names with
 their counts, and flags collective kernels: the atta IPC kernels (``oneshot_kernel`` sums,
 ``keymax_kernel`` sampler MAX) vs RCCL (``nccl``/``rccl``) - the evidence that a TP decode
@@ -37,12 +38,11 @@ def short(name: str) -> str:
 
 
 def summarise(path: Path) -> str:
-    text = path.read_text(errors="replace")
-    kinds = collections.Counter(m.lower() for m in re.findall(
-        r"\b(KERNEL|MEMCPY|MEMSET|HOST|EVENT_RECORD|WAIT_EVENT|EMPTY|GRAPH)\b", text, re.I))
-    mangled = re.findall(r"(_Z[0-9A-Za-z_]+)", text)
-    dm = demangle(sorted(set(mangled)))
-    kern = collections.Counter(short(dm.get(m, m)) for m in mangled)
+    lines = [x for x in path.read_text(errors="replace").splitlines() if x.strip()]
+    kinds = collections.Counter(x.split(":", 1)[0] for x in lines)
+    names = [x.split(":", 1)[1].split(" grid=")[0] for x in lines if x.startswith("kernel:")]
+    dm = demangle(sorted({n for n in names if n.startswith("_Z")}))
+    kern = collections.Counter(short(dm.get(n, n)) for n in names)
     lines = [f"== {path.name}: node kinds {dict(kinds)}"]
     for k, c in kern.most_common():
         tag = ""
@@ -60,9 +60,9 @@ def summarise(path: Path) -> str:
 
 def main(argv: list[str]) -> int:
     root = Path(argv[1] if len(argv) > 1 else "gpurun_out/graphs")
-    files = sorted(root.glob("*.dot"))
+    files = sorted(root.glob("*.nodes"))
     if not files:
-        print(f"no .dot files under {root}")
+        print(f"no .nodes files under {root}")
         return 1
     for f in files:
         print(summarise(f))
