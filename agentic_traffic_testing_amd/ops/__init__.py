@@ -496,6 +496,49 @@ def linear_fp8(x: torch.Tensor, q: torch.Tensor, scale: torch.Tensor) -> torch.T
     return gemm_fp8(xq, xs, q, scale, x.dtype)
 
 
+GEMM_PLAIN, GEMM_RESADD, GEMM_SILU = 0, 1, 2
+
+
+def prefill_gemm_ok(x: torch.Tensor, w: torch.Tensor, mode: int = GEMM_PLAIN) -> bool:
+    """Shapes the hand-written prefill GEMM (ops/csrc/prefill_gemm.hip) takes: bf16, K a
+    multiple of 32, output width a multiple of 256 (128 for the SiLU mode), 16-B aligned
+    rows."""
+    n = w.shape[0] // 2 if mode == GEMM_SILU else w.shape[0]
+    return (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 2
+            and x.shape[1] == w.shape[1] and x.shape[1] % 32 == 0 and x.stride(1) == 1
+            and x.stride(0) % 8 == 0 and w.is_contiguous()
+            and n % (128 if mode == GEMM_SILU else 256) == 0)
+
+
+def prefill_gemm(x: torch.Tensor, w: torch.Tensor, mode: int = GEMM_PLAIN,
+                 residual: torch.Tensor | None = None,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+    """Hand-written CDNA4 prefill GEMM: ``x @ w.T`` (GEMM_PLAIN), ``residual += x @ w.T`` in
+    place (GEMM_RESADD; returns ``residual``) or ``silu(x @ gate.T) * (x @ up.T)`` for
+    ``w = [gate; up]`` (GEMM_SILU).  fp32 accumulate, one rounding.  CPU tensors run the
+    PyTorch reference of the same op."""
+    n = w.shape[0] // 2 if mode == GEMM_SILU else w.shape[0]
+    if not x.is_cuda:
+        y = x.float() @ w.float().t()
+        if mode == GEMM_SILU:
+            y = torch.nn.functional.silu(y[:, :n]) * y[:, n:]
+        if mode == GEMM_RESADD:
+            residual.copy_((y + residual.float()).to(residual.dtype))
+            return residual
+        y = y.to(x.dtype)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    if mode == GEMM_RESADD:
+        _native().prefill_gemm(residual, x, w, residual, mode)
+        return residual
+    if out is None:
+        out = torch.empty(x.shape[0], n, dtype=x.dtype, device=x.device)
+    _native().prefill_gemm(out, x, w, None, mode)
+    return out
+
+
 def _need_cuda(x, preshuffled):
     if preshuffled and not x.is_cuda:
         raise ValueError("pre-shuffled weights are only consumed by the HIP decode kernels")

@@ -306,6 +306,35 @@ void skinny_gemm(at::Tensor y, const at::Tensor& x, const at::Tensor& w,
            "skinny_gemm");
 }
 
+// c = a . w^T (mode 0), c = res + a . w^T (mode 1, res may alias c), c = silu(a . gate^T) *
+// (a . up^T) with w = [gate; up] (mode 2): the hand-written CDNA4 prefill GEMM.
+void prefill_gemm(at::Tensor c, const at::Tensor& a, const at::Tensor& w,
+                  const c10::optional<at::Tensor>& residual, int64_t mode) {
+  check_dev(a, "a");
+  TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && c.dim() == 2, "prefill_gemm: 2-D operands");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
+                  c.scalar_type() == at::kBFloat16,
+              "prefill_gemm: bf16 operands");
+  TORCH_CHECK(a.stride(1) == 1 && w.stride(1) == 1 && c.stride(1) == 1, "prefill_gemm: layout");
+  const int64_t n = mode == 2 ? w.size(0) / 2 : w.size(0);
+  TORCH_CHECK(a.size(1) == w.size(1) && c.size(0) == a.size(0) && c.size(1) == n &&
+                  (mode != 2 || w.size(0) % 2 == 0),
+              "prefill_gemm: shapes");
+  const void* r = nullptr;
+  int64_t rs = 0;
+  if (mode == 1) {
+    TORCH_CHECK(residual.has_value() && residual->defined() && residual->sizes() == c.sizes() &&
+                    residual->stride(1) == 1 && residual->scalar_type() == at::kBFloat16,
+                "prefill_gemm: residual");
+    r = residual->data_ptr();
+    rs = residual->stride(0);
+  }
+  const at::DeviceGuard g(a.device());
+  check_rc(atta_prefill_gemm(c.data_ptr(), a.data_ptr(), w.data_ptr(), r, a.size(0), n, a.size(1),
+                             a.stride(0), w.stride(0), c.stride(0), rs, mode, cur_stream()),
+           "prefill_gemm");
+}
+
 void check_skinny(const at::Tensor& x, const at::Tensor& w, const char* what) {
   TORCH_CHECK(w.size(0) % 16 == 0 && w.size(1) % 32 == 0, what, ": weight tile shape");
   check_dev(x, "x");
@@ -770,6 +799,7 @@ TORCH_LIBRARY(atta, m) {
   m.def("sample_finalize(Tensor(a!) tokens, Tensor keys, int n_tiles) -> ()");
   m.def("skinny_gemm(Tensor(a!) y, Tensor x, Tensor w, Tensor? residual, int waves, "
         "bool preshuffled=False, Tensor? w_scale=None, int ksplit=1) -> ()");
+  m.def("prefill_gemm(Tensor(a!) c, Tensor a, Tensor w, Tensor? residual, int mode) -> ()");
   m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rms_norm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");
@@ -814,6 +844,7 @@ TORCH_LIBRARY_IMPL(atta, CUDA, m) {
   m.impl("sample", &sample);
   m.impl("sample_topkp", &sample_topkp);
   m.impl("skinny_gemm", &skinny_gemm);
+  m.impl("prefill_gemm", &prefill_gemm);
   m.impl("fused_qkv_rope", &fused_qkv_rope);
   m.impl("fused_gate_up_silu", &fused_gate_up_silu);
   m.impl("fused_lm_head_sample", &fused_lm_head_sample);

@@ -20,7 +20,7 @@
 //   * ring: 16 slots of 8 KiB, slot = seq & 15 for the workgroup's chunk sequence; chunk
 //     seq is consumed by wave seq & 7, so each wave owns two alternating slots.  FULL /
 //     FREE generation words in LDS: the loader publishes a slot behind a counted vmcnt that
-//     keeps the next kInFlight chunks in flight; a wave releases a slot as soon as its 8 KiB
+//     keeps its newest chunks in flight (several loader waves: ~112 KiB per CU); a wave releases a slot as soon as its 8 KiB
 //     are in registers (before the MFMAs).
 //   * activations (x) are read by the compute waves straight from global memory with
 //     device-scope (sc1) buffer loads, one chunk ahead; the norm's sum of squares comes from
@@ -43,6 +43,7 @@
 // Scope: TP = 1, 16-bit pre-shuffled weights, K dims multiples of 2048 (H, I, NQ*128),
 // GQA group <= 4, <= 16 rows, 128-token partitions; the model runner falls back to the
 // per-kernel decode path otherwise.
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <string>
@@ -54,7 +55,8 @@ namespace atta {
 namespace mk {
 
 constexpr int kCW = 8;                    // compute waves
-constexpr int kThreads = (kCW + 1) * 64;  // + the loader wave
+constexpr int kMaxLoaders = 4;
+constexpr int kThreads = (kCW + kMaxLoaders) * 64;  // + up to 4 loader waves
 constexpr int kSlots = 16;                // ring slots (2 per compute wave)
 constexpr int kSlotBytes = 8192;          // 8 MFMA blocks of 1 KiB
 constexpr int kRows = 16;                 // MFMA M (rows >= p.M are zero)
@@ -64,10 +66,7 @@ constexpr int kCtrStride = 16;            // uint32 words between counter shards
 constexpr int kMaxG = 4;                  // GQA group
 constexpr int kPartTokens = kCW * 16;     // attention partition = 8 waves x 16 tokens
 constexpr unsigned kSpinLimit = 1u << 24;
-// chunks the loader keeps in flight before publishing one (vmcnt counts 1 KiB DMAs): 2 chunks
-// = 16 KiB per CU in flight measured 6.3 ms per 8B decode step (~2.4 TB/s: latency-bound)
-constexpr int kInFlight = 6;
-static_assert(8 * kInFlight <= 63, "vmcnt field");
+
 
 // error word bits
 constexpr unsigned kErrPoll = 1u, kErrFull = 2u, kErrFree = 4u, kErrBar = 8u;
@@ -81,6 +80,7 @@ struct LayerW {
 
 struct Params {
   int M, H, I, V, L, NQ, NKV, G;
+  int nloaders, inflight;  // loader waves, chunks each keeps in flight
   int bt_stride, bs_shift, max_parts;
   float eps, scale_log2;
   const LayerW* layers;
@@ -286,13 +286,35 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_dst) {
       : "memory");
 }
 
-__device__ void loader(PP pp, Shared& sh, unsigned* err) {
+// s_waitcnt vmcnt needs an immediate: keep the loader's newest `f` chunks (8 DMAs each) in
+// flight, f in 1..7
+__device__ __forceinline__ void wait_chunks_in_flight(int f) {
+  switch (f) {
+    case 1: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
+  }
+}
+
+// Loader wave r of p.nloaders: streams every chunk seq with seq % nloaders == r into ring slot
+// seq & 15 and publishes it once its DMAs landed, keeping its newest p.inflight chunks in
+// flight (the latency of a streaming HBM read under full load is ~4-5 us, so a CU needs
+// ~128 KiB in flight: one wave's vmcnt window (<= 7 chunks) cannot hold that, several
+// loader waves can).  Deadlock-free while inflight * nloaders < kSlots - 1: publishing chunk
+// n then only needs slots freed by chunks < n.
+__device__ void loader(PP pp, Shared& sh, unsigned* err, int r) {
   const auto& p = *pp;
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.x;
+  const int nl = p.nloaders, F = p.inflight;
   const uint32_t ring0 = __builtin_amdgcn_readfirstlane(
       static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sh.ring)));
-  uint32_t seq = 0;
+  uint32_t seq = 0;        // workgroup chunk sequence
+  uint32_t mine = 0;       // chunks this loader issued
   unsigned long long free_wait = 0;
   const unsigned long long t_begin = __builtin_amdgcn_s_memtime();
   auto publish = [&](uint32_t s) {
@@ -308,7 +330,8 @@ __device__ void loader(PP pp, Shared& sh, unsigned* err) {
     for (int i = 0; i < nt; ++i) {
       const uint16_t* tb = ph.w + static_cast<int64_t>(c + i * p.G) * tile_elems;
       for (int j = 0; j < nch; ++j) {
-        for (int w = 0; w < kCW; ++w) {
+        for (int w = 0; w < kCW; ++w, ++seq) {
+          if (static_cast<int>(seq % nl) != r) continue;
           const int slot = seq & (kSlots - 1);
           const unsigned gen = (seq >> 4) + 1;
           if (gen > 1 && ld_volatile(&sh.freed[slot]) + 1 < gen) {
@@ -328,18 +351,24 @@ __device__ void loader(PP pp, Shared& sh, unsigned* err) {
 #pragma unroll
           for (int u = 0; u < 8; ++u)
             dma16(src + u * 512, __builtin_amdgcn_readfirstlane(dst + u * 1024));
-          if (seq >= kInFlight) {
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 * kInFlight) : "memory");
-            publish(seq - kInFlight);
+          ++mine;
+          if (static_cast<int>(mine) > F) {
+            wait_chunks_in_flight(F);
+            publish(seq - static_cast<uint32_t>(F * nl));
           }
-          ++seq;
         }
       }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  for (uint32_t s = seq > kInFlight ? seq - kInFlight : 0; s < seq; ++s) publish(s);
-  if (p.stats != nullptr && lane == 0) {
+  // publish this loader's last min(F, mine) chunks (seq now = total chunks)
+  const uint32_t total = seq;
+  for (int k = 0; k < F; ++k) {
+    if (static_cast<int>(mine) - 1 - k < 0) break;
+    const uint32_t s_ = static_cast<uint32_t>(r) + static_cast<uint32_t>(mine - 1 - k) * nl;
+    if (s_ < total) publish(s_);
+  }
+  if (p.stats != nullptr && lane == 0 && r == 0) {
     p.stats[blockIdx.x * 4 + 0] = free_wait;
     p.stats[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memtime() - t_begin;
   }
@@ -825,8 +854,8 @@ __global__ void __launch_bounds__(kThreads, 1) decode_step_kernel(const Params* 
     if (p.stats != nullptr) p.stats[blockIdx.x * 4 + 3] = 0;
   }
   __syncthreads();  // the only s_barrier: before the roles split
-  if (wave == kCW) {
-    loader(pp, sh, err);
+  if (wave >= kCW) {
+    loader(pp, sh, err, wave - kCW);
     return;
   }
   // row ids (token of each row: the previous step's device sample under look-ahead)
@@ -1000,7 +1029,20 @@ int atta_decode_step(const DecodeStepArgs& a, hipStream_t stream) {
   if (a.max_parts < 1 || a.max_parts > 64) return -1;
   const int grid = atta_decode_step_grid();
   if (grid <= 0) return -1;
+  static const int nload = [] {
+    const char* e = std::getenv("ATTA_MK_LOADERS");
+    return e ? std::atoi(e) : 2;
+  }();
+  static const int infl = [] {
+    const char* e = std::getenv("ATTA_MK_INFLIGHT");
+    return e ? std::atoi(e) : 7;
+  }();
+  if (nload < 1 || nload > mk::kMaxLoaders || infl < 1 || infl > 7 ||
+      infl * nload > mk::kSlots - 2)
+    return -1;
   mk::Params p{};
+  p.nloaders = nload;
+  p.inflight = infl;
   p.M = a.M;
   p.H = a.H;
   p.I = a.I;
@@ -1045,10 +1087,11 @@ int atta_decode_step(const DecodeStepArgs& a, hipStream_t stream) {
   p.stats = g_mk_stats;
   const mk::Params* dp = mk::device_params(p, stream);
   if (dp == nullptr) return -3;  // first use of this parameter block while capturing
+  const int threads = (mk::kCW + nload) * 64;
   switch (G) {
-    case 1: mk::decode_step_kernel<1><<<grid, mk::kThreads, 0, stream>>>(dp); break;
-    case 2: mk::decode_step_kernel<2><<<grid, mk::kThreads, 0, stream>>>(dp); break;
-    default: mk::decode_step_kernel<4><<<grid, mk::kThreads, 0, stream>>>(dp); break;
+    case 1: mk::decode_step_kernel<1><<<grid, threads, 0, stream>>>(dp); break;
+    case 2: mk::decode_step_kernel<2><<<grid, threads, 0, stream>>>(dp); break;
+    default: mk::decode_step_kernel<4><<<grid, threads, 0, stream>>>(dp); break;
   }
   return static_cast<int>(hipGetLastError());
 }

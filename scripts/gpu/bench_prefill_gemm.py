@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""A/B of the hand-written CDNA4 prefill GEMM (ops.prefill_gemm) against hipBLASLt
+(torch F.linear / addmm) on the Llama-3.1-8B prefill projections, cold weights (4 rotating
+copies so every call streams W from HBM, as in a real prefill), uniform random operands.
+
+Reports per shape: us per call and dense TF/s (2*M*N*K; the SILU row counts both gate and up
+columns).  The gate_up rows compare the fused SiLU-mul GEMM against hipBLASLt gate_up +
+the silu_and_mul kernel (what the prefill path runs without it).
+
+    python scripts/gpu/bench_prefill_gemm.py --m 512 1300 2600 > profiles/r3_prefill_gemm_ab.txt
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+from agentic_traffic_testing_amd import ops  # noqa: E402
+
+SHAPES = {  # name: (N rows of W, K, mode)
+    "qkv": (6144, 4096, ops.GEMM_PLAIN),
+    "o+res": (4096, 4096, ops.GEMM_RESADD),
+    "gate_up+silu": (28672, 4096, ops.GEMM_SILU),
+    "down+res": (4096, 14336, ops.GEMM_RESADD),
+}
+
+
+def timed(fn, iters):
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn(0)
+    e0.record()
+    for i in range(iters):
+        fn(i)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", type=int, nargs="+", default=[512, 1300, 2600])
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--copies", type=int, default=4)
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    dev = "cuda"
+    print(f"# prefill GEMM A/B, {torch.cuda.get_device_name()}, cold weights x{args.copies}, "
+          f"random operands; TF/s = 2*M*N*K / t")
+    for name, (n, k, mode) in SHAPES.items():
+        if args.only and args.only not in name:
+            continue
+        ws = [(torch.rand(n, k, device=dev) * 2 - 1).to(torch.bfloat16) / k ** 0.5
+              for _ in range(args.copies)]
+        for m in args.m:
+            x = (torch.rand(m, k, device=dev) * 2 - 1).to(torch.bfloat16)
+            nout = n // 2 if mode == ops.GEMM_SILU else n
+            res = torch.randn(m, nout, device=dev).to(torch.bfloat16)
+            out = torch.empty(m, nout, device=dev, dtype=torch.bfloat16)
+            flops = 2.0 * m * n * k
+
+            def ours(i):
+                w = ws[i % len(ws)]
+                if mode == ops.GEMM_RESADD:
+                    ops.prefill_gemm(x, w, mode, residual=res)
+                else:
+                    ops.prefill_gemm(x, w, mode, out=out)
+
+            def blas(i):
+                w = ws[i % len(ws)]
+                if mode == ops.GEMM_RESADD:
+                    res.addmm_(x, w.t())
+                elif mode == ops.GEMM_SILU:
+                    ops.silu_and_mul(torch.nn.functional.linear(x, w))
+                else:
+                    torch.nn.functional.linear(x, w)
+
+            # numerics spot check against hipBLASLt (fp32 accumulate both)
+            ref = torch.nn.functional.linear(x, ws[0]).float()
+            if mode == ops.GEMM_SILU:
+                ref = torch.nn.functional.silu(ref[:, :nout]) * ref[:, nout:]
+                got = ops.prefill_gemm(x, ws[0], mode).float()
+            else:
+                got = ops.prefill_gemm(x, ws[0]).float()
+            err = ((got - ref).abs().max() / ref.abs().max()).item()
+            t_ours = timed(ours, args.iters)
+            t_blas = timed(blas, args.iters)
+            print(f"{name:13s} M={m:5d} N={n:6d} K={k:6d} | atta {t_ours:8.1f} us "
+                  f"{flops / t_ours / 1e6:7.0f} TF | hipBLASLt {t_blas:8.1f} us "
+                  f"{flops / t_blas / 1e6:7.0f} TF | speedup {t_blas / t_ours:5.2f}x "
+                  f"| rel err {err:.2e}", flush=True)
+        del ws
+
+
+if __name__ == "__main__":
+    main()

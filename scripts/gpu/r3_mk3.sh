@@ -1,0 +1,12 @@
+#!/bin/bash
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+OUT=gpurun_out; mkdir -p $OUT
+run() { local name=$1 t=$2; shift 2; echo "=== $name"; timeout -k 10 $t "$@" > $OUT/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; tail -${TAILN:-8} $OUT/$name.log; if [ $rc -ne 0 ]; then echo STOP; exit $rc; fi; }
+TAILN=6 run r3_gemm_tests 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_prefill_gemm.py
+TAILN=20 run r3_gemm_ab 400 python scripts/gpu/bench_prefill_gemm.py --m 512 1300 2600
+TAILN=6 run r3_mk_tests3 400 python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests/test_engine.py -k "megakernel"
+for cfg in "2 7" "4 3" "1 7"; do set -- $cfg
+  ATTA_MK_LOADERS=$1 ATTA_MK_INFLIGHT=$2 TAILN=14 run r3_mk_prof_L$1_F$2 300 python scripts/gpu/mk_profile.py --steps 24 --rows 1 5
+done

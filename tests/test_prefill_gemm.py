@@ -1,0 +1,79 @@
+"""Hand-written CDNA4 prefill GEMM (ops/csrc/prefill_gemm.hip) vs a plain PyTorch fp32
+reference of the same op: plain, residual-add (in place) and SiLU-mul (w = [gate; up])
+epilogues, ragged M (row clamping at the last tile), K not a multiple of the 4-phase ring."""
+import pytest
+import torch
+
+from agentic_traffic_testing_amd import ops
+
+
+def _ref(x, w, mode, res=None):
+    y = x.float() @ w.float().t()
+    if mode == ops.GEMM_SILU:
+        n = w.shape[0] // 2
+        y = torch.nn.functional.silu(y[:, :n]) * y[:, n:]
+    if mode == ops.GEMM_RESADD:
+        y = y + res.float()
+    return y
+
+
+def _check(got, exp, k):
+    # bf16 output rounding (2^-8 relative) + fp32 accumulation-order noise
+    err = (got.float() - exp).abs()
+    tol = 2e-2 * exp.abs() + 2e-3 * k ** 0.5
+    assert bool((err <= tol).all()), f"max err {err.max().item():.4g}"
+
+
+def test_prefill_gemm_cpu_reference_path():
+    torch.manual_seed(0)
+    x = torch.randn(5, 64, dtype=torch.bfloat16)
+    w = torch.randn(512, 64, dtype=torch.bfloat16) / 8
+    assert ops.prefill_gemm_ok(x, w) and ops.prefill_gemm_ok(x, w, ops.GEMM_SILU)
+    assert not ops.prefill_gemm_ok(x, w[:300])
+    _check(ops.prefill_gemm(x, w), _ref(x, w, ops.GEMM_PLAIN), 64)
+    _check(ops.prefill_gemm(x, w, ops.GEMM_SILU), _ref(x, w, ops.GEMM_SILU), 64)
+    r = torch.randn(5, 512, dtype=torch.bfloat16)
+    exp = _ref(x, w, ops.GEMM_RESADD, r)
+    assert ops.prefill_gemm(x, w, ops.GEMM_RESADD, residual=r) is r
+    _check(r, exp, 64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mnk", [(1, 256, 32), (77, 512, 96), (256, 256, 256),
+                                 (300, 768, 4096), (1029, 1024, 1056), (2600, 512, 4096)])
+def test_prefill_gemm_vs_fp32(mode, mnk):
+    assert ops.native_available(), ops._load_error
+    M, N, K = mnk
+    torch.manual_seed(M + N + K + mode)
+    dev = "cuda"
+    x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    rows = 2 * N if mode == ops.GEMM_SILU else N
+    w = (torch.randn(rows, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+    if mode == ops.GEMM_RESADD:
+        r = torch.randn(M, N, device=dev).to(torch.bfloat16)
+        exp = _ref(x, w, mode, r)
+        got = ops.prefill_gemm(x, w, mode, residual=r)
+        assert got is r
+    else:
+        exp = _ref(x, w, mode)
+        got = ops.prefill_gemm(x, w, mode)
+    torch.cuda.synchronize()
+    assert got.shape == (M, N)
+    _check(got, exp, K)
+
+
+@pytest.mark.gpu
+def test_prefill_gemm_strided_rows_and_asymmetric_operands():
+    """A with a row stride (a view into a wider buffer) and an asymmetric W: catches a
+    transposed C/D map or a wrong swizzle on either side (guide §5 'Common mistakes' 3)."""
+    assert ops.native_available(), ops._load_error
+    torch.manual_seed(7)
+    M, N, K = 333, 512, 1024
+    big = torch.randn(M, K + 64, device="cuda").to(torch.bfloat16)
+    x = big[:, 32:32 + K]
+    w = (torch.arange(N * K, device="cuda").reshape(N, K) % 97 - 48).to(torch.bfloat16) / 64
+    _check(ops.prefill_gemm(x, w), _ref(x, w, ops.GEMM_PLAIN), K)
+    eye = torch.eye(K, device="cuda", dtype=torch.bfloat16)[:256]
+    got = ops.prefill_gemm(x, eye)
+    assert torch.equal(got, x[:, :256])
