@@ -500,43 +500,60 @@ GEMM_PLAIN, GEMM_RESADD, GEMM_SILU = 0, 1, 2
 
 
 def prefill_gemm_ok(x: torch.Tensor, w: torch.Tensor, mode: int = GEMM_PLAIN) -> bool:
-    """Shapes the hand-written prefill GEMM (ops/csrc/prefill_gemm.hip) takes: bf16, K a
-    multiple of 32, output width a multiple of 256 (128 for the SiLU mode), 16-B aligned
-    rows."""
+    """Shapes the hand-written prefill GEMM (ops/csrc/prefill_gemm.hip) takes: bf16 or fp8
+    (uint8 e4m3fn) operands, K a multiple of 64 bytes, output width a multiple of 256 (128
+    for the SiLU mode), 16-B aligned rows."""
     n = w.shape[0] // 2 if mode == GEMM_SILU else w.shape[0]
-    return (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 2
-            and x.shape[1] == w.shape[1] and x.shape[1] % 32 == 0 and x.stride(1) == 1
-            and x.stride(0) % 8 == 0 and w.is_contiguous()
+    el = x.element_size()
+    return (x.dtype in (torch.bfloat16, torch.uint8) and w.dtype == x.dtype and x.dim() == 2
+            and x.shape[1] == w.shape[1] and (x.shape[1] * el) % 64 == 0 and x.stride(1) == 1
+            and (x.stride(0) * el) % 16 == 0 and w.is_contiguous()
             and n % (128 if mode == GEMM_SILU else 256) == 0)
 
 
 def prefill_gemm(x: torch.Tensor, w: torch.Tensor, mode: int = GEMM_PLAIN,
-                 residual: torch.Tensor | None = None,
-                 out: torch.Tensor | None = None) -> torch.Tensor:
+                 residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
+                 xs: torch.Tensor | None = None, ws: torch.Tensor | None = None) -> torch.Tensor:
     """Hand-written CDNA4 prefill GEMM: ``x @ w.T`` (GEMM_PLAIN), ``residual += x @ w.T`` in
     place (GEMM_RESADD; returns ``residual``) or ``silu(x @ gate.T) * (x @ up.T)`` for
-    ``w = [gate; up]`` (GEMM_SILU).  fp32 accumulate, one rounding.  CPU tensors run the
-    PyTorch reference of the same op."""
+    ``w = [gate; up]`` (GEMM_SILU).  bf16 operands, or fp8: uint8 e4m3fn ``x`` / ``w`` with
+    fp32 row scales ``xs`` [M, 1] / ``ws`` [rows of w] (applied in the epilogue).  fp32
+    accumulate, one rounding to bf16.  CPU tensors run the PyTorch reference of the op."""
     n = w.shape[0] // 2 if mode == GEMM_SILU else w.shape[0]
+    fp8 = x.dtype == torch.uint8
+    if fp8 and (xs is None or ws is None):
+        raise ValueError("prefill_gemm: fp8 operands need row scales xs and ws")
     if not x.is_cuda:
-        y = x.float() @ w.float().t()
+        if fp8:
+            xf = x.view(torch.float8_e4m3fn).float() * xs.reshape(-1, 1)
+            wf = w.view(torch.float8_e4m3fn).float() * ws.reshape(-1, 1)
+        else:
+            xf, wf = x.float(), w.float()
+        y = xf @ wf.t()
         if mode == GEMM_SILU:
             y = torch.nn.functional.silu(y[:, :n]) * y[:, n:]
         if mode == GEMM_RESADD:
             residual.copy_((y + residual.float()).to(residual.dtype))
             return residual
-        y = y.to(x.dtype)
+        y = y.to(torch.bfloat16)
         if out is not None:
             out.copy_(y)
             return out
         return y
+    xs_ = xs.reshape(-1) if fp8 else None
+    ws_ = ws.reshape(-1) if fp8 else None
     if mode == GEMM_RESADD:
-        _native().prefill_gemm(residual, x, w, residual, mode)
+        _native().prefill_gemm(residual, x, w, residual, mode, xs_, ws_)
         return residual
     if out is None:
-        out = torch.empty(x.shape[0], n, dtype=x.dtype, device=x.device)
-    _native().prefill_gemm(out, x, w, None, mode)
+        out = torch.empty(x.shape[0], n, dtype=torch.bfloat16, device=x.device)
+    _native().prefill_gemm(out, x, w, None, mode, xs_, ws_)
     return out
+
+
+def prefill_gemm_error() -> int:
+    """Nonzero once a stream-K finisher of the prefill GEMM timed out waiting for a partial."""
+    return int(_native().prefill_gemm_error())
 
 
 def _need_cuda(x, preshuffled):

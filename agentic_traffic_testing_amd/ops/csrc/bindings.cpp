@@ -307,19 +307,32 @@ void skinny_gemm(at::Tensor y, const at::Tensor& x, const at::Tensor& w,
 }
 
 // c = a . w^T (mode 0), c = res + a . w^T (mode 1, res may alias c), c = silu(a . gate^T) *
-// (a . up^T) with w = [gate; up] (mode 2): the hand-written CDNA4 prefill GEMM.
+// (a . up^T) with w = [gate; up] (mode 2): the hand-written CDNA4 prefill GEMM.  bf16 a / w, or
+// uint8 (e4m3fn) a / w with fp32 row scales xs [M, 1] / ws [rows of w].
 void prefill_gemm(at::Tensor c, const at::Tensor& a, const at::Tensor& w,
-                  const c10::optional<at::Tensor>& residual, int64_t mode) {
+                  const c10::optional<at::Tensor>& residual, int64_t mode,
+                  const c10::optional<at::Tensor>& xs, const c10::optional<at::Tensor>& ws) {
   check_dev(a, "a");
   TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && c.dim() == 2, "prefill_gemm: 2-D operands");
-  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
-                  c.scalar_type() == at::kBFloat16,
-              "prefill_gemm: bf16 operands");
+  const bool fp8 = a.scalar_type() == at::kByte;
+  TORCH_CHECK(c.scalar_type() == at::kBFloat16 && w.scalar_type() == a.scalar_type() &&
+                  (fp8 || a.scalar_type() == at::kBFloat16),
+              "prefill_gemm: bf16 or fp8 (uint8) operands, bf16 output");
   TORCH_CHECK(a.stride(1) == 1 && w.stride(1) == 1 && c.stride(1) == 1, "prefill_gemm: layout");
   const int64_t n = mode == 2 ? w.size(0) / 2 : w.size(0);
   TORCH_CHECK(a.size(1) == w.size(1) && c.size(0) == a.size(0) && c.size(1) == n &&
                   (mode != 2 || w.size(0) % 2 == 0),
               "prefill_gemm: shapes");
+  const float* xsp = nullptr;
+  const float* wsp = nullptr;
+  if (fp8) {
+    TORCH_CHECK(xs.has_value() && ws.has_value() && xs->scalar_type() == at::kFloat &&
+                    ws->scalar_type() == at::kFloat && xs->is_contiguous() &&
+                    ws->is_contiguous() && xs->numel() == a.size(0) && ws->numel() == w.size(0),
+                "prefill_gemm: fp8 needs fp32 row scales xs [M] and ws [rows of w]");
+    xsp = xs->data_ptr<float>();
+    wsp = ws->data_ptr<float>();
+  }
   const void* r = nullptr;
   int64_t rs = 0;
   if (mode == 1) {
@@ -331,9 +344,12 @@ void prefill_gemm(at::Tensor c, const at::Tensor& a, const at::Tensor& w,
   }
   const at::DeviceGuard g(a.device());
   check_rc(atta_prefill_gemm(c.data_ptr(), a.data_ptr(), w.data_ptr(), r, a.size(0), n, a.size(1),
-                             a.stride(0), w.stride(0), c.stride(0), rs, mode, cur_stream()),
+                             a.stride(0), w.stride(0), c.stride(0), rs, mode, fp8 ? 1 : 0, xsp,
+                             wsp, cur_stream()),
            "prefill_gemm");
 }
+
+int64_t prefill_gemm_error() { return atta_prefill_gemm_error(); }
 
 void check_skinny(const at::Tensor& x, const at::Tensor& w, const char* what) {
   TORCH_CHECK(w.size(0) % 16 == 0 && w.size(1) % 32 == 0, what, ": weight tile shape");
@@ -799,7 +815,8 @@ TORCH_LIBRARY(atta, m) {
   m.def("sample_finalize(Tensor(a!) tokens, Tensor keys, int n_tiles) -> ()");
   m.def("skinny_gemm(Tensor(a!) y, Tensor x, Tensor w, Tensor? residual, int waves, "
         "bool preshuffled=False, Tensor? w_scale=None, int ksplit=1) -> ()");
-  m.def("prefill_gemm(Tensor(a!) c, Tensor a, Tensor w, Tensor? residual, int mode) -> ()");
+  m.def("prefill_gemm(Tensor(a!) c, Tensor a, Tensor w, Tensor? residual, int mode, Tensor? xs=None, Tensor? ws=None) -> ()");
+  m.def("prefill_gemm_error() -> int", &prefill_gemm_error);
   m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rms_norm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");

@@ -168,8 +168,10 @@ int atta_decode_step_grid();
 // profiling buffers of later persistent-step launches (nullptr: off): see decode_step.hip
 void atta_set_decode_step_trace(void* trace, void* stats);
 
-// Prefill GEMM (prefill_gemm.hip): c[M, N] = a[M, K] . w[N, K]^T (bf16); mode 0 plain,
-// 1 c = res + a.w^T (res may alias c), 2 c = silu(a.gate^T) * (a.up^T) with w = [gate; up].
+// Prefill GEMM (prefill_gemm.hip): c[M, N] = a[M, K] . w[N, K]^T; mode 0 plain, 1 c = res +
+// a.w^T (res may alias c), 2 c = silu(a.gate^T) * (a.up^T) with w = [gate; up].  fp8: a / w are
+// e4m3fn bytes with fp32 row scales xs [M] / wsc [rows of w]; else bf16.
 int atta_prefill_gemm(void* c, const void* a, const void* w, const void* res, int M, int N,
                       int K, int64_t lda, int64_t ldw, int64_t ldc, int64_t ldres, int mode,
-                      hipStream_t stream);
+                      int fp8, const float* xs, const float* wsc, hipStream_t stream);
+int atta_prefill_gemm_error();

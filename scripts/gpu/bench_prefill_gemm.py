@@ -46,17 +46,26 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--copies", type=int, default=4)
     ap.add_argument("--only", default="")
+    ap.add_argument("--fp8", action="store_true",
+                    help="e4m3fn operands with row scales: ours vs hipBLASLt torch._scaled_mm")
     args = ap.parse_args()
     dev = "cuda"
-    print(f"# prefill GEMM A/B, {torch.cuda.get_device_name()}, cold weights x{args.copies}, "
-          f"random operands; TF/s = 2*M*N*K / t")
+    print(f"# prefill GEMM A/B ({'fp8 e4m3fn, row scales' if args.fp8 else 'bf16'}), "
+          f"{torch.cuda.get_device_name()}, cold weights x{args.copies}, random operands; "
+          f"TF/s = 2*M*N*K / t; stream-K error word checked at the end")
     for name, (n, k, mode) in SHAPES.items():
         if args.only and args.only not in name:
             continue
         ws = [(torch.rand(n, k, device=dev) * 2 - 1).to(torch.bfloat16) / k ** 0.5
               for _ in range(args.copies)]
+        if args.fp8:
+            qs = [ops.quant_rows_fp8(w) for w in ws]
+            ws = [q for q, _ in qs]
+            wsc = [s.reshape(-1).contiguous() for _, s in qs]
         for m in args.m:
             x = (torch.rand(m, k, device=dev) * 2 - 1).to(torch.bfloat16)
+            if args.fp8:
+                x, xs = ops.quant_rows_fp8(x)
             nout = n // 2 if mode == ops.GEMM_SILU else n
             res = torch.randn(m, nout, device=dev).to(torch.bfloat16)
             out = torch.empty(m, nout, device=dev, dtype=torch.bfloat16)
@@ -64,27 +73,37 @@ def main():
 
             def ours(i):
                 w = ws[i % len(ws)]
+                kw = dict(xs=xs, ws=wsc[i % len(ws)]) if args.fp8 else {}
                 if mode == ops.GEMM_RESADD:
-                    ops.prefill_gemm(x, w, mode, residual=res)
+                    ops.prefill_gemm(x, w, mode, residual=res, **kw)
                 else:
-                    ops.prefill_gemm(x, w, mode, out=out)
+                    ops.prefill_gemm(x, w, mode, out=out, **kw)
+
+            def lin(i):
+                w = ws[i % len(ws)]
+                if args.fp8:
+                    return ops.gemm_fp8(x, xs, w, wsc[i % len(ws)])
+                return torch.nn.functional.linear(x, w)
 
             def blas(i):
-                w = ws[i % len(ws)]
                 if mode == ops.GEMM_RESADD:
-                    res.addmm_(x, w.t())
+                    if args.fp8:
+                        res.add_(lin(i))
+                    else:
+                        res.addmm_(x, ws[i % len(ws)].t())
                 elif mode == ops.GEMM_SILU:
-                    ops.silu_and_mul(torch.nn.functional.linear(x, w))
+                    ops.silu_and_mul(lin(i))
                 else:
-                    torch.nn.functional.linear(x, w)
+                    lin(i)
 
             # numerics spot check against hipBLASLt (fp32 accumulate both)
-            ref = torch.nn.functional.linear(x, ws[0]).float()
+            ref = lin(0).float()
+            kw = dict(xs=xs, ws=wsc[0]) if args.fp8 else {}
             if mode == ops.GEMM_SILU:
                 ref = torch.nn.functional.silu(ref[:, :nout]) * ref[:, nout:]
-                got = ops.prefill_gemm(x, ws[0], mode).float()
+                got = ops.prefill_gemm(x, ws[0], mode, **kw).float()
             else:
-                got = ops.prefill_gemm(x, ws[0]).float()
+                got = ops.prefill_gemm(x, ws[0], **kw).float()
             err = ((got - ref).abs().max() / ref.abs().max()).item()
             t_ours = timed(ours, args.iters)
             t_blas = timed(blas, args.iters)
@@ -93,6 +112,7 @@ def main():
                   f"{flops / t_blas / 1e6:7.0f} TF | speedup {t_blas / t_ours:5.2f}x "
                   f"| rel err {err:.2e}", flush=True)
         del ws
+    assert ops.prefill_gemm_error() == 0, "stream-K finisher timed out"
 
 
 if __name__ == "__main__":

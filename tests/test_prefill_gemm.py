@@ -77,3 +77,77 @@ def test_prefill_gemm_strided_rows_and_asymmetric_operands():
     eye = torch.eye(K, device="cuda", dtype=torch.bfloat16)[:256]
     got = ops.prefill_gemm(x, eye)
     assert torch.equal(got, x[:, :256])
+
+
+def _q8(t):
+    """Row-wise e4m3fn quantisation: (uint8 codes, fp32 scales [rows, 1])."""
+    s = (t.float().abs().amax(dim=1, keepdim=True) / 448.0).clamp_min(1e-12)
+    q = (t.float() / s).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
+    return q, s
+
+
+def _ref8(xq, xs, wq, ws, mode, res=None):
+    x = xq.view(torch.float8_e4m3fn).float() * xs.reshape(-1, 1)
+    w = wq.view(torch.float8_e4m3fn).float() * ws.reshape(-1, 1)
+    y = x @ w.t()
+    if mode == ops.GEMM_SILU:
+        n = w.shape[0] // 2
+        y = torch.nn.functional.silu(y[:, :n]) * y[:, n:]
+    if mode == ops.GEMM_RESADD:
+        y = y + res.float()
+    return y
+
+
+def test_prefill_gemm_fp8_cpu_reference_path():
+    torch.manual_seed(3)
+    xq, xs = _q8(torch.randn(7, 128))
+    wq, ws = _q8(torch.randn(256, 128))
+    assert ops.prefill_gemm_ok(xq, wq)
+    _check(ops.prefill_gemm(xq, wq, xs=xs, ws=ws), _ref8(xq, xs, wq, ws, 0), 128)
+    with pytest.raises(ValueError):
+        ops.prefill_gemm(xq, wq)
+
+
+@pytest.mark.gpu
+def test_prefill_gemm_fp8_exact_integer_layout():
+    """Small integers are exact in e4m3 and their products sum exactly in fp32: any error
+    in the 32x32x64 f8f6f4 operand or C/D lane maps, or in the LDS swizzle, shows up as a
+    mismatch (guide: 'check the map with exact integer data')."""
+    assert ops.native_available(), ops._load_error
+    M, N, K = 300, 512, 256
+    g = torch.Generator().manual_seed(11)
+    xi = torch.randint(-3, 4, (M, K), generator=g).float()
+    wi = torch.randint(-3, 4, (N, K), generator=g).float()
+    wi[:, :64] += torch.arange(N).reshape(-1, 1) % 5  # asymmetric W
+    xq = xi.to(torch.float8_e4m3fn).view(torch.uint8).cuda()
+    wq = wi.to(torch.float8_e4m3fn).view(torch.uint8).cuda()
+    ones_m = torch.ones(M, 1, device="cuda")
+    ones_n = torch.ones(N, device="cuda")
+    got = ops.prefill_gemm(xq, wq, xs=ones_m, ws=ones_n).float().cpu()
+    exp = (xi @ wi.t()).to(torch.bfloat16).float()
+    assert torch.equal(got, exp), f"{(got != exp).sum().item()} mismatches"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mnk", [(1, 256, 64), (77, 512, 192), (300, 768, 4096),
+                                 (1029, 1024, 1088), (2600, 512, 4096)])
+def test_prefill_gemm_fp8_vs_fp32(mode, mnk):
+    assert ops.native_available(), ops._load_error
+    M, N, K = mnk
+    torch.manual_seed(M + N + K + 10 * mode)
+    rows = 2 * N if mode == ops.GEMM_SILU else N
+    xq, xs = _q8(torch.randn(M, K, device="cuda"))
+    wq, ws = _q8(torch.randn(rows, K, device="cuda") / K ** 0.5)
+    ws = ws.reshape(-1).contiguous()
+    if mode == ops.GEMM_RESADD:
+        r = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+        exp = _ref8(xq, xs, wq, ws, mode, r)
+        got = ops.prefill_gemm(xq, wq, mode, residual=r, xs=xs, ws=ws)
+    else:
+        exp = _ref8(xq, xs, wq, ws, mode)
+        got = ops.prefill_gemm(xq, wq, mode, xs=xs, ws=ws)
+    torch.cuda.synchronize()
+    assert got.shape == (M, N)
+    _check(got, exp, K)
+    assert ops.prefill_gemm_error() == 0
