@@ -117,6 +117,8 @@ class ModelRunner:
         t0 = time.perf_counter()
         self.model = LlamaModel(model_cfg, self.dtype, self.device, tp_rank, tp_size, comm,
                                 quantization=cfg.quantization)
+        self.model.prefill_gemm = cfg.prefill_gemm
+        self.model.prefill_gemm_min_rows = cfg.prefill_gemm_min_rows
         if weights_dir and cfg.load_format != "dummy":
             self.model.load_safetensors(weights_dir)
         else:

@@ -84,6 +84,10 @@ class LlamaModel:
         if quantization not in ("", "fp8"):
             raise ValueError(f"unsupported quantization {quantization!r}")
         self.quant = quantization
+        # prefill projections: "hipblaslt" (torch / hipBLASLt GEMMs) or "atta" (the
+        # hand-written CDNA4 GEMM, ops/csrc/prefill_gemm.hip) for >= prefill_gemm_min_rows rows
+        self.prefill_gemm = "hipblaslt"
+        self.prefill_gemm_min_rows = 128
         self.cfg = cfg
         self.dtype = dtype
         self.device = torch.device(device)
@@ -333,7 +337,9 @@ class LlamaModel:
                 else:
                     xq, xs = ops.quant_rows_fp8(pending, ops.QUANT_ADDNORM, L.input_norm, eps,
                                                 residual)
-                qkv = ops.gemm_fp8(xq, xs, L.qkv, L.qkv_s, dt)
+                qkv = self._gemm8(xq, xs, L.qkv, L.qkv_s, dt)
+            elif self._pg(T, L.qkv):
+                qkv = ops.prefill_gemm(ops.rms_norm(residual, L.input_norm, eps), L.qkv)
             else:
                 qkv = self._proj(ops.rms_norm(residual, L.input_norm, eps), L.qkv, L.qkv_s)
             q = ops.rope_cache(qkv, md.positions, md.slot_mapping, self.cos_sin, k_caches[li],
@@ -349,16 +355,24 @@ class LlamaModel:
                                       self.scale, out=attn)
             if fp8:
                 aq, as_ = ops.quant_rows_fp8(attn.view(T, nq * D))
-                y = self._all_reduce(ops.gemm_fp8(aq, as_, L.o, L.o_s, dt))
+                y = self._all_reduce(self._gemm8(aq, as_, L.o, L.o_s, dt))
                 xq, xs = ops.quant_rows_fp8(y, ops.QUANT_ADDNORM, L.post_norm, eps, residual)
-                gu = ops.gemm_fp8(xq, xs, L.gate_up, L.gate_up_s, dt)
-                aq, as_ = ops.quant_rows_fp8(gu, ops.QUANT_SILU)
-                pending = self._all_reduce(ops.gemm_fp8(aq, as_, L.down, L.down_s, dt))
+                if self._pg(T, xq, L.gate_up, ops.GEMM_SILU):
+                    # SiLU-mul fused into the gate_up GEMM epilogue: [T, I] out, plain quant
+                    act = ops.prefill_gemm(xq, L.gate_up, ops.GEMM_SILU, xs=xs, ws=L.gate_up_s)
+                    aq, as_ = ops.quant_rows_fp8(act)
+                else:
+                    gu = ops.gemm_fp8(xq, xs, L.gate_up, L.gate_up_s, dt)
+                    aq, as_ = ops.quant_rows_fp8(gu, ops.QUANT_SILU)
+                pending = self._all_reduce(self._gemm8(aq, as_, L.down, L.down_s, dt))
                 continue
             self._proj_residual(attn.view(T, nq * D), L.o, L.o_s, residual)
             x = ops.rms_norm(residual, L.post_norm, eps)
-            gu = self._proj(x, L.gate_up, L.gate_up_s)
-            a = ops.silu_and_mul(gu)
+            if self._pg(T, L.gate_up, mode=ops.GEMM_SILU):
+                a = ops.prefill_gemm(x, L.gate_up, ops.GEMM_SILU)
+            else:
+                gu = self._proj(x, L.gate_up, L.gate_up_s)
+                a = ops.silu_and_mul(gu)
             self._proj_residual(a, L.down, L.down_s, residual)
         if rows is not None:
             residual = residual.index_select(0, rows)
@@ -367,8 +381,33 @@ class LlamaModel:
             return ops.fused_add_rms_norm(pending, residual, self.norm, eps)
         return ops.rms_norm(residual, self.norm, eps)
 
+    def _pg(self, T: int, *ops_, mode: int = 0) -> bool:
+        """Route this prefill projection to the hand-written CDNA4 GEMM (ops.prefill_gemm):
+        ``prefill_gemm == "atta"``, at least ``prefill_gemm_min_rows`` rows, shapes it takes.
+        Called as _pg(T, w) for bf16 (activation shape implied) or _pg(T, xq, w, mode)."""
+        if self.prefill_gemm != "atta" or T < self.prefill_gemm_min_rows:
+            return False
+        if self.device.type != "cuda":
+            return False
+        if len(ops_) == 1:
+            w = ops_[0]
+            x = torch.empty_strided((T, w.shape[1]), (w.shape[1], 1), dtype=w.dtype, device="meta")
+            return ops.prefill_gemm_ok(x, w, mode)
+        return ops.prefill_gemm_ok(ops_[0], ops_[1], mode)
+
+    def _gemm8(self, xq, xs, w, ws, dt):
+        """fp8 prefill projection: the hand-written fp8 GEMM when routed there, else the
+        hipBLASLt row-scaled GEMM."""
+        if self._pg(xq.shape[0], xq, w):
+            return ops.prefill_gemm(xq, w, xs=xs, ws=ws)
+        return ops.gemm_fp8(xq, xs, w, ws, dt)
+
     def _proj_residual(self, x, w, scale, residual):
         """residual += x @ w.T (row-parallel projection; TP: all-reduced partial sums)."""
+        if scale is None and self._pg(x.shape[0], x, w, ops.GEMM_RESADD):
+            if self.tp_size > 1:
+                return self.tp_group.all_reduce_residual(ops.prefill_gemm(x, w), residual)
+            return ops.prefill_gemm(x, w, ops.GEMM_RESADD, residual=residual)
         if self.tp_size > 1:
             # residual += sum over ranks, the add fused into the IPC reduction's epilogue
             return self.tp_group.all_reduce_residual(self._proj(x, w, scale), residual)

@@ -1030,12 +1030,12 @@ int atta_decode_step(const DecodeStepArgs& a, hipStream_t stream) {
   const int grid = atta_decode_step_grid();
   if (grid <= 0) return -1;
   static const int nload = [] {
-    const char* e = std::getenv("ATTA_MK_LOADERS");
-    return e ? std::atoi(e) : 2;
+    const char* e = std::getenv("ATTA_MK_LOADERS");  // 4 x 3 measured best of 1x7, 2x7, 4x3
+    return e ? std::atoi(e) : 4;                      // (profiles/r3_megakernel_timeline_*)
   }();
   static const int infl = [] {
     const char* e = std::getenv("ATTA_MK_INFLIGHT");
-    return e ? std::atoi(e) : 7;
+    return e ? std::atoi(e) : 3;
   }();
   if (nload < 1 || nload > mk::kMaxLoaders || infl < 1 || infl > 7 ||
       infl * nload > mk::kSlots - 2)

@@ -451,8 +451,9 @@ def _check_fp8(eng, prompts, n, tol_logit):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("prefill_gemm", ["hipblaslt", "atta"])
 @pytest.mark.parametrize("model", ["small", "llama-70b-slice"])
-def test_fp8_engine_matches_fp32_oracle(model):
+def test_fp8_engine_matches_fp32_oracle(model, prefill_gemm):
     """greedy tokens of the fp8 engine (fp8 prefill GEMMs with per-token
     activation quantisation, weight-only fp8 decode GEMVs, graphs) against an fp32 dense
     oracle on the dequantised weights with the prefill rows' activation quantisation emulated
@@ -460,8 +461,29 @@ def test_fp8_engine_matches_fp32_oracle(model):
     vocab = 30000 if model == "small" else 16000
     cfg = EngineConfig(model=model, device="cuda", max_model_len=512, num_kv_blocks=512,
                        max_num_batched_tokens=128, max_num_seqs=8,
-                       graph_batch_sizes=(1, 2, 4, 8), quantization="fp8")
+                       graph_batch_sizes=(1, 2, 4, 8), quantization="fp8",
+                       prefill_gemm=prefill_gemm, prefill_gemm_min_rows=1)
     eng = LLMEngine(cfg)
     outs, bad = _check_fp8(eng, _prompts(vocab=vocab), n=8, tol_logit=0.3)
     assert bad <= 2
     assert eng.runner.graph_steps > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", ["small", "llama-8b-slice"])
+def test_prefill_gemm_engine_matches_oracle(model):
+    """Prefill projections on the hand-written CDNA4 GEMM (ops/csrc/prefill_gemm.hip: qkv
+    plain, o / down residual-add, gate_up with the SiLU-mul epilogue) against the fp32 dense
+    oracle (near-tie rule), plus the Stream-K fix-up error word."""
+    vocab = 30000 if model == "small" else 16000
+    cfg = EngineConfig(model=model, device="cuda", max_model_len=1024, num_kv_blocks=512,
+                       max_num_batched_tokens=512, max_num_seqs=8,
+                       graph_batch_sizes=(1, 2, 4, 8), prefill_gemm="atta",
+                       prefill_gemm_min_rows=1)
+    eng = LLMEngine(cfg)
+    prompts = _prompts(vocab=vocab)
+    prompts.append(list(np.random.default_rng(5).integers(300, vocab, size=600)))
+    outs, bad = _check(eng, prompts, n=6, tol_logit=0.25)
+    assert bad <= 2
+    from agentic_traffic_testing_amd import ops
+    assert ops.prefill_gemm_error() == 0
