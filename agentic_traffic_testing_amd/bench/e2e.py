@@ -173,6 +173,19 @@ def run_e2e(engine, steps: int, warmup: int, fanout: int = 5, max_tokens: int = 
                 os.environ[k] = v
     tokens = sum(int(r["completion_tokens"]) for r in recs)
     ttfts = sorted(float(r["queue_wait_s"]) for r in recs)
+
+    def med(xs):
+        xs = [float(x) for x in xs]
+        return round(statistics.median(xs), 4) if xs else None
+
+    # TTFT split: fan-out (burst) requests vs solo calls, and the part of a burst request's
+    # TTFT spent held for its siblings (burst-aware admission)
+    breakdown = {
+        "burst_calls": sum(1 for r in recs if r.get("burst")),
+        "p50_ttft_burst_s": med(r["queue_wait_s"] for r in recs if r.get("burst")),
+        "p50_ttft_solo_s": med(r["queue_wait_s"] for r in recs if not r.get("burst")),
+        "p50_hold_burst_s": med(r.get("hold_s", 0.0) for r in recs if r.get("burst")),
+    }
     return {
         "workload": workload,
         "tokens": tokens,
@@ -185,4 +198,5 @@ def run_e2e(engine, steps: int, warmup: int, fanout: int = 5, max_tokens: int = 
         "p50_ttft_s": statistics.median(ttfts) if ttfts else None,
         "p95_ttft_s": ttfts[min(len(ttfts) - 1, int(0.95 * len(ttfts)))] if ttfts else None,
         "per_task_s": [round(d, 3) for d in per_task],
+        "ttft_breakdown": breakdown,
     }

@@ -212,10 +212,11 @@ class EngineConfig:
     # (X-Task-ID + x-fanout headers) are held up to this long for their siblings so the
     # burst shares one prefill; 0 disables.  Requests without the headers are never held.
     burst_window_ms: float = 10.0
-    # prefill projection GEMMs: "hipblaslt" or "atta" (hand-written CDNA4 Stream-K GEMM with
-    # fused residual-add / SiLU-mul epilogues, bf16 and fp8: ops/csrc/prefill_gemm.hip) for
-    # steps of >= prefill_gemm_min_rows tokens
-    prefill_gemm: str = "hipblaslt"
+    # prefill projection GEMMs: "hipblaslt", "atta" (hand-written CDNA4 Stream-K GEMM with
+    # fused residual-add / SiLU-mul epilogues, bf16 and fp8: ops/csrc/prefill_gemm.hip, for
+    # steps of >= prefill_gemm_min_rows tokens) or "auto" (each projection on whichever won
+    # the measured A/B at that size: models/llama.py LlamaModel._PG_AUTO)
+    prefill_gemm: str = "auto"
     prefill_gemm_min_rows: int = 128
     # async look-ahead decode: launch the next decode graph step before waiting for the
     # current one's tokens (llm_engine.LLMEngine.step)

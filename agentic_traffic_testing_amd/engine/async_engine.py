@@ -48,6 +48,8 @@ class AsyncEngine:
         # late sibling is admitted at once instead of opening a new window
         self._flushed: dict[str, list] = {}
         self.bursts_coalesced = 0  # groups admitted together (complete or at the deadline)
+        # request id -> seconds its burst held it (popped by the server into its records)
+        self.hold_s: dict[str, float] = {}
         self.on_step = on_step
         # intermediate outputs of a request are coalesced to at most one per interval (the
         # first token and the final output always go out at once): every delivery wakes the
@@ -185,7 +187,10 @@ class AsyncEngine:
                 del self._held[key]
                 if len(group) < size:
                     self._flushed[key] = [size - len(group), now + 30.0]
+                if len(self.hold_s) > 4096:  # callers that never pop: stay bounded
+                    self.hold_s.clear()
                 for entry in group:  # arrival order: FIFO admission within the burst
+                    self.hold_s[entry[0]] = max(0.0, now - entry[3])
                     self._admit(entry)
                 self.bursts_coalesced += 1
             elif nearest is None or deadline < nearest:

@@ -86,7 +86,7 @@ class LlamaModel:
         self.quant = quantization
         # prefill projections: "hipblaslt" (torch / hipBLASLt GEMMs) or "atta" (the
         # hand-written CDNA4 GEMM, ops/csrc/prefill_gemm.hip) for >= prefill_gemm_min_rows rows
-        self.prefill_gemm = "hipblaslt"
+        self.prefill_gemm = "auto"
         self.prefill_gemm_min_rows = 128
         self.cfg = cfg
         self.dtype = dtype
@@ -337,8 +337,8 @@ class LlamaModel:
                 else:
                     xq, xs = ops.quant_rows_fp8(pending, ops.QUANT_ADDNORM, L.input_norm, eps,
                                                 residual)
-                qkv = self._gemm8(xq, xs, L.qkv, L.qkv_s, dt)
-            elif self._pg(T, L.qkv):
+                qkv = self._gemm8(xq, xs, L.qkv, L.qkv_s, dt, "qkv")
+            elif self._pg(T, L.qkv, proj="qkv"):
                 qkv = ops.prefill_gemm(ops.rms_norm(residual, L.input_norm, eps), L.qkv)
             else:
                 qkv = self._proj(ops.rms_norm(residual, L.input_norm, eps), L.qkv, L.qkv_s)
@@ -355,25 +355,25 @@ class LlamaModel:
                                       self.scale, out=attn)
             if fp8:
                 aq, as_ = ops.quant_rows_fp8(attn.view(T, nq * D))
-                y = self._all_reduce(self._gemm8(aq, as_, L.o, L.o_s, dt))
+                y = self._all_reduce(self._gemm8(aq, as_, L.o, L.o_s, dt, "o"))
                 xq, xs = ops.quant_rows_fp8(y, ops.QUANT_ADDNORM, L.post_norm, eps, residual)
-                if self._pg(T, xq, L.gate_up, ops.GEMM_SILU):
+                if self._pg(T, xq, L.gate_up, mode=ops.GEMM_SILU, proj="gate_up"):
                     # SiLU-mul fused into the gate_up GEMM epilogue: [T, I] out, plain quant
                     act = ops.prefill_gemm(xq, L.gate_up, ops.GEMM_SILU, xs=xs, ws=L.gate_up_s)
                     aq, as_ = ops.quant_rows_fp8(act)
                 else:
                     gu = ops.gemm_fp8(xq, xs, L.gate_up, L.gate_up_s, dt)
                     aq, as_ = ops.quant_rows_fp8(gu, ops.QUANT_SILU)
-                pending = self._all_reduce(self._gemm8(aq, as_, L.down, L.down_s, dt))
+                pending = self._all_reduce(self._gemm8(aq, as_, L.down, L.down_s, dt, "down"))
                 continue
-            self._proj_residual(attn.view(T, nq * D), L.o, L.o_s, residual)
+            self._proj_residual(attn.view(T, nq * D), L.o, L.o_s, residual, "o")
             x = ops.rms_norm(residual, L.post_norm, eps)
-            if self._pg(T, L.gate_up, mode=ops.GEMM_SILU):
+            if self._pg(T, L.gate_up, mode=ops.GEMM_SILU, proj="gate_up"):
                 a = ops.prefill_gemm(x, L.gate_up, ops.GEMM_SILU)
             else:
                 gu = self._proj(x, L.gate_up, L.gate_up_s)
                 a = ops.silu_and_mul(gu)
-            self._proj_residual(a, L.down, L.down_s, residual)
+            self._proj_residual(a, L.down, L.down_s, residual, "down")
         if rows is not None:
             residual = residual.index_select(0, rows)
             pending = None if pending is None else pending.index_select(0, rows)
@@ -381,13 +381,26 @@ class LlamaModel:
             return ops.fused_add_rms_norm(pending, residual, self.norm, eps)
         return ops.rms_norm(residual, self.norm, eps)
 
-    def _pg(self, T: int, *ops_, mode: int = 0) -> bool:
+    # "auto" routing of the prefill projections: (weight dtype, mode) -> the smallest row count
+    # from which the hand-written GEMM beat hipBLASLt in the cold-weight A/B on the 8B shapes
+    # (profiles/r3_prefill_gemm_ab_*: fp8 gate_up+SiLU 1.03-1.19x from M 512, fp8 down 1.10-1.13x
+    # at M 2600, bf16 gate_up+SiLU 1.06-1.10x at M 2600; everything else stays on hipBLASLt)
+    _PG_AUTO = {(torch.uint8, "gate_up"): 512, (torch.uint8, "down"): 2048,
+                (torch.bfloat16, "gate_up"): 2048}
+
+    def _pg(self, T: int, *ops_, mode: int = 0, proj: str = "") -> bool:
         """Route this prefill projection to the hand-written CDNA4 GEMM (ops.prefill_gemm):
-        ``prefill_gemm == "atta"``, at least ``prefill_gemm_min_rows`` rows, shapes it takes.
-        Called as _pg(T, w) for bf16 (activation shape implied) or _pg(T, xq, w, mode)."""
-        if self.prefill_gemm != "atta" or T < self.prefill_gemm_min_rows:
-            return False
+        ``prefill_gemm == "atta"`` (from ``prefill_gemm_min_rows`` rows) or ``"auto"`` (the
+        measured winners, _PG_AUTO), for shapes it takes.  Called as _pg(T, w) for bf16
+        (activation shape implied) or _pg(T, xq, w, mode)."""
         if self.device.type != "cuda":
+            return False
+        w = ops_[-1]
+        if self.prefill_gemm == "auto":
+            m = self._PG_AUTO.get((w.dtype, proj))
+            if m is None or T < m:
+                return False
+        elif self.prefill_gemm != "atta" or T < self.prefill_gemm_min_rows:
             return False
         if len(ops_) == 1:
             w = ops_[0]
@@ -395,16 +408,16 @@ class LlamaModel:
             return ops.prefill_gemm_ok(x, w, mode)
         return ops.prefill_gemm_ok(ops_[0], ops_[1], mode)
 
-    def _gemm8(self, xq, xs, w, ws, dt):
+    def _gemm8(self, xq, xs, w, ws, dt, proj=""):
         """fp8 prefill projection: the hand-written fp8 GEMM when routed there, else the
         hipBLASLt row-scaled GEMM."""
-        if self._pg(xq.shape[0], xq, w):
+        if self._pg(xq.shape[0], xq, w, proj=proj):
             return ops.prefill_gemm(xq, w, xs=xs, ws=ws)
         return ops.gemm_fp8(xq, xs, w, ws, dt)
 
-    def _proj_residual(self, x, w, scale, residual):
+    def _proj_residual(self, x, w, scale, residual, proj=""):
         """residual += x @ w.T (row-parallel projection; TP: all-reduced partial sums)."""
-        if scale is None and self._pg(x.shape[0], x, w, ops.GEMM_RESADD):
+        if scale is None and self._pg(x.shape[0], x, w, mode=ops.GEMM_RESADD, proj=proj):
             if self.tp_size > 1:
                 return self.tp_group.all_reduce_residual(ops.prefill_gemm(x, w), residual)
             return ops.prefill_gemm(x, w, ops.GEMM_RESADD, residual=residual)

@@ -551,6 +551,14 @@ def prefill_gemm(x: torch.Tensor, w: torch.Tensor, mode: int = GEMM_PLAIN,
     return out
 
 
+def prefill_gemm_config(schedule: str = "hybrid", group_m: int = 4, ablate: int = 0) -> None:
+    """Tile schedule of the prefill GEMM: "hybrid" (data-parallel rounds + Stream-K
+    remainder), "streamk" or "dp"; ``group_m`` M tiles per raster group; ``ablate``
+    (measurement only, bf16 plain GEMMs): 1 no MFMA, 2 no LDS-DMA, 3 no ds_read."""
+    _native().prefill_gemm_config({"hybrid": 0, "streamk": 1, "dp": 2}[schedule], group_m,
+                                  ablate)
+
+
 def prefill_gemm_error() -> int:
     """Nonzero once a stream-K finisher of the prefill GEMM timed out waiting for a partial."""
     return int(_native().prefill_gemm_error())

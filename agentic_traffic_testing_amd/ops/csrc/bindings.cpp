@@ -350,6 +350,11 @@ void prefill_gemm(at::Tensor c, const at::Tensor& a, const at::Tensor& w,
 }
 
 int64_t prefill_gemm_error() { return atta_prefill_gemm_error(); }
+void prefill_gemm_config(int64_t schedule, int64_t group_m, int64_t ablate) {
+  check_rc(atta_prefill_gemm_config(static_cast<int>(schedule), static_cast<int>(group_m),
+                                    static_cast<int>(ablate)),
+           "prefill_gemm_config");
+}
 
 void check_skinny(const at::Tensor& x, const at::Tensor& w, const char* what) {
   TORCH_CHECK(w.size(0) % 16 == 0 && w.size(1) % 32 == 0, what, ": weight tile shape");
@@ -817,6 +822,7 @@ TORCH_LIBRARY(atta, m) {
         "bool preshuffled=False, Tensor? w_scale=None, int ksplit=1) -> ()");
   m.def("prefill_gemm(Tensor(a!) c, Tensor a, Tensor w, Tensor? residual, int mode, Tensor? xs=None, Tensor? ws=None) -> ()");
   m.def("prefill_gemm_error() -> int", &prefill_gemm_error);
+  m.def("prefill_gemm_config(int schedule, int group_m, int ablate=0) -> ()", &prefill_gemm_config);
   m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rms_norm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");
   m.def("silu_and_mul(Tensor(a!) out, Tensor x) -> ()");

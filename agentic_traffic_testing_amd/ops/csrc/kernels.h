@@ -175,3 +175,4 @@ int atta_prefill_gemm(void* c, const void* a, const void* w, const void* res, in
                       int K, int64_t lda, int64_t ldw, int64_t ldc, int64_t ldres, int mode,
                       int fp8, const float* xs, const float* wsc, hipStream_t stream);
 int atta_prefill_gemm_error();
+int atta_prefill_gemm_config(int schedule, int group_m, int ablate);

@@ -313,7 +313,8 @@ async def handle_chat(request: web.Request) -> web.Response:
                    f"{prompt_tokens} completion_tokens={completion_tokens}")
         st.records.append({"t_end": time.time(), "queue_wait_s": queue_wait,
                            "prompt_tokens": prompt_tokens,
-                           "completion_tokens": completion_tokens, "burst": burst})
+                           "completion_tokens": completion_tokens, "burst": burst,
+                           "hold_s": st.aengine.hold_s.pop(request_id, 0.0)})
         meta = {
             "request_id": request_id,
             "latency_ms": latency_ms,

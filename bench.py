@@ -64,6 +64,19 @@ def overrides(items: list[str]) -> dict:
     return out
 
 
+def _window_marker(a):
+    """ATTA_WINDOW_MARKERS=1: one tiny stream_read_kernel dispatch at each edge of the timed
+    region, so a rocprof kernel trace can be windowed to it (scripts/gpu/summarize_trace.py
+    --window stream_read_kernel): init, weight generation and warm-up stay out of the table.
+    Outside the timed interval (launched after t_start is read / after elapsed is taken)."""
+    if a.device != "cuda" or os.environ.get("ATTA_WINDOW_MARKERS", "0") != "1":
+        return
+    buf = torch.zeros(4096, dtype=torch.int32, device="cuda")
+    sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+    torch.ops.atta.stream_read(buf, sink)
+    torch.cuda.synchronize()
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -207,12 +220,14 @@ def main_dp(a, world: int):
     if dist:
         dist.barrier()
     _sync(a)
+    _window_marker(a)
     t_start = time.perf_counter()
     results = [wl.run_episode() for _ in range(a.steps)]
     _sync(a)
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    _window_marker(a)
 
     if a.verbose and rank == 0:
         tm = eng.timing
@@ -326,6 +341,7 @@ def _finish_http(a, eng, world, rank, dist, init_s, cfg, log):
             "p95_ttft_s": round(p95, 4) if p95 is not None else None,
             "llm_calls": r["calls"], "llm_calls_per_workflow": r["calls_per_workflow"],
             "peak_inflight": r["peak_inflight"], "bursts_coalesced": r["bursts_coalesced"],
+            "ttft_breakdown": r.get("ttft_breakdown"),
             "completion_tokens": int(tokens),
             "per_task_s": r["per_task_s"], "init_s": round(init_s, 1)}), flush=True)
     if dist:

@@ -48,11 +48,15 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--fp8", action="store_true",
                     help="e4m3fn operands with row scales: ours vs hipBLASLt torch._scaled_mm")
+    ap.add_argument("--schedule", default="hybrid", choices=["hybrid", "streamk", "dp"])
+    ap.add_argument("--group-m", type=int, default=4)
     args = ap.parse_args()
+    ops.prefill_gemm_config(args.schedule, args.group_m)
     dev = "cuda"
     print(f"# prefill GEMM A/B ({'fp8 e4m3fn, row scales' if args.fp8 else 'bf16'}), "
           f"{torch.cuda.get_device_name()}, cold weights x{args.copies}, random operands; "
-          f"TF/s = 2*M*N*K / t; stream-K error word checked at the end")
+          f"TF/s = 2*M*N*K / t; schedule {args.schedule}, group_m {args.group_m}; "
+          f"stream-K error word checked at the end")
     for name, (n, k, mode) in SHAPES.items():
         if args.only and args.only not in name:
             continue

@@ -31,16 +31,29 @@ def main():
     eng = LLMEngine(cfg)
     rng = np.random.default_rng(0)
     sp = SamplingParams(temperature=0.2, max_tokens=1, ignore_eos=True)
+    # window markers for rocprof summaries (scripts/gpu/summarize_trace.py --window): one
+    # stream_read_kernel dispatch brackets each measured (post-warm-up) region, so model init,
+    # random-weight generation and the warm-up prefill never enter a profile table
+    buf = torch.zeros(4096, dtype=torch.int32, device="cuda")
+    sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+    def marker():
+        torch.ops.atta.stream_read(buf, sink)
+        torch.cuda.synchronize()
+
     for n in map(int, a.tokens.split(",")):
         times = []
         for r in range(a.reps + 1):
             prompt = rng.integers(1000, 100000, size=n).tolist()
             torch.cuda.synchronize()
+            if r == 1:
+                marker()
             t0 = time.perf_counter()
             eng.generate([prompt], sp)
             torch.cuda.synchronize()
             if r:
                 times.append((time.perf_counter() - t0) * 1e3)
+        marker()
         print(f"prefill {n:6d} tokens: {statistics.median(times):8.2f} ms "
               f"({n / statistics.median(times) * 1e3:9.0f} tok/s)", flush=True)
 

@@ -10,7 +10,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -
   > gpurun_out/prof_prefill.log 2>&1
 rc=$?
 echo "rc=$rc"; cat gpurun_out/prof_prefill.log | grep prefill
-python3 scripts/gpu/summarize_trace.py $OUT > gpurun_out/prof_prefill_summary.txt 2>&1
+python3 scripts/gpu/summarize_trace.py $OUT --window stream_read_kernel > gpurun_out/prof_prefill_summary.txt 2>&1
 head -45 gpurun_out/prof_prefill_summary.txt
 python3 scripts/gpu/trace_window.py $OUT sample_kernel 45 > gpurun_out/prof_prefill_window.txt 2>&1
 find $OUT -name "*kernel_trace.csv" -delete

@@ -6,19 +6,36 @@ import os
 import sys
 from collections import defaultdict
 
+# usage: summarize_trace.py DIR [--window MARKER]
+# --window: only the dispatches strictly between the first and the last dispatch of a kernel
+# whose name contains MARKER (e.g. stream_read_kernel, which scripts/gpu/prefill_bench.py
+# launches around its measured region): model init and warm-up stay out of the table.
 d = sys.argv[1]
+window = sys.argv[sys.argv.index("--window") + 1] if "--window" in sys.argv else None
 files = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
 if not files:
     print("no kernel trace found"); sys.exit(0)
-tot = defaultdict(float); cnt = defaultdict(int)
-rows = []
+raw = []
 for f in files:
     with open(f) as fh:
         for r in csv.DictReader(fh):
-            name = r.get("Kernel_Name", "?")
-            dt = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-            tot[name] += dt; cnt[name] += 1
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
+            raw.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                        r.get("Kernel_Name", "?")))
+raw.sort()
+if window:
+    idx = [i for i, r in enumerate(raw) if window in r[2]]
+    if len(idx) >= 2:
+        raw = raw[idx[0] + 1:idx[-1]]
+        raw = [r for r in raw if window not in r[2]]
+        print(f"window: dispatches between the first and last {window} ({len(raw)} kernels)")
+    else:
+        print(f"window marker {window} not found twice: whole trace")
+tot = defaultdict(float); cnt = defaultdict(int)
+rows = []
+for s_, e_, name in raw:
+    dt = (e_ - s_) / 1e3
+    tot[name] += dt; cnt[name] += 1
+    rows.append((s_, e_, name))
 all_t = sum(tot.values())
 print(f"kernels: {sum(cnt.values())} dispatches, {all_t/1e3:.1f} ms total GPU time")
 print(f"{'total_ms':>10} {'calls':>8} {'avg_us':>9} {'pct':>6}  kernel")

@@ -93,7 +93,12 @@ def dense_logits_fp8(model, ids, n_prompt):
         a = _qdq_rows(a.reshape(T, -1).to(model.dtype).float(), P)
         x = (x + a @ deq(L.o, L.o_s).t()).to(model.dtype).float()
         h = _qdq_rows(ref.rms_norm(x, L.post_norm.float(), c.rms_norm_eps), P)
-        g = ref.silu_and_mul((h @ deq(L.gate_up, L.gate_up_s).t()).to(model.dtype).float())
+        gu = h @ deq(L.gate_up, L.gate_up_s).t()
+        if getattr(model, "prefill_gemm", "") != "atta":
+            gu = gu.to(model.dtype).float()
+        else:  # the fused SiLU-mul GEMM epilogue: prefill rows see fp32 gate / up values
+            gu = torch.cat([gu[:P], gu[P:].to(model.dtype).float()])
+        g = ref.silu_and_mul(gu)
         g = _qdq_rows(g.to(model.dtype).float(), P)
         x = (x + g @ deq(L.down, L.down_s).t()).to(model.dtype).float()
     x = ref.rms_norm(x, model.norm.float(), c.rms_norm_eps)
