@@ -81,6 +81,9 @@ struct LayerW {
 struct Params {
   int M, H, I, V, L, NQ, NKV, G;
   int nloaders, inflight;  // loader waves, chunks each keeps in flight
+  int plain;               // EXPERIMENT ONLY (ATTA_MK_PLAIN_LOADS=1): x / q / K / V read through
+                           // the L2 without sc1 - may read stale lines; timing probe of what a
+                           // write-once-buffer design would gain
   int bt_stride, bs_shift, max_parts;
   float eps, scale_log2;
   const LayerW* layers;
@@ -153,8 +156,15 @@ struct Shared {
 typedef const __attribute__((address_space(4))) Params* PP;  // constant address space:
                                                               // scalar (s_load) reads
 __device__ __forceinline__ PP fresh(PP p) {
-  asm volatile("" : "+s"(p));
-  return p;
+  // readfirstlane first: the value is then provably uniform for the "s" constraint even
+  // where the divergence analysis loses track of it (after loops with divergent exits)
+  const uint64_t v = (uint64_t)p;
+  // (readfirstlane returns int: widen through uint32_t, never sign-extend the low half)
+  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32)));
+  const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v)));
+  uint64_t u = (static_cast<uint64_t>(hi) << 32) | static_cast<uint64_t>(lo);
+  asm volatile("" : "+s"(u));
+  return (PP)u;
 }
 
 // Same for the LDS block: per-lane LDS addresses derived from a laundered base are computed
@@ -162,8 +172,9 @@ __device__ __forceinline__ PP fresh(PP p) {
 // them stay live across the layer loop and spill).
 __device__ __forceinline__ Shared& fresh_lds(Shared& s) {
   __attribute__((address_space(3))) Shared* p = (__attribute__((address_space(3))) Shared*)&s;
-  asm volatile("" : "+s"(p));
-  return *(Shared*)p;
+  uint32_t u = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)p));
+  asm volatile("" : "+s"(u));
+  return *(Shared*)(__attribute__((address_space(3))) Shared*)(uintptr_t)u;
 }
 
 __device__ __forceinline__ unsigned ld_volatile(const unsigned* p) {
@@ -436,7 +447,9 @@ __device__ void gemv_phase(PP pp, Shared& sh_, int layer, const XSrc& xs,
         xf[u] = *reinterpret_cast<const frag8*>(xs.erow + k);
       } else {
         const uint32_t off = static_cast<uint32_t>((col * xs.row_stride + k) * 2);
-        xf[u] = __builtin_bit_cast(frag8, dev_load16(xs.rs, off));
+        xf[u] = __builtin_bit_cast(
+            frag8, p.plain ? __builtin_amdgcn_raw_buffer_load_b128(xs.rs, off, 0, 0)
+                           : dev_load16(xs.rs, off));
       }
     }
   };
@@ -649,7 +662,9 @@ __device__ void attention_phase(PP pp, Shared& sh_, int layer, unsigned* err) {
           (static_cast<int64_t>(s) * p.NQ * kD + (hk * G + (ok ? col : 0)) * kD + 32 * grp) * 2);
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk)
-        qf[kk] = ok ? __builtin_bit_cast(frag8, dev_load16(rq, off + kk * 16)) : frag8{};
+        qf[kk] = ok ? __builtin_bit_cast(frag8, p.plain ? __builtin_amdgcn_raw_buffer_load_b128(rq, off + kk * 16, 0, 0)
+                                                        : dev_load16(rq, off + kk * 16))
+                    : frag8{};
     }
     f32x4 o[8];
 #pragma unroll
@@ -663,11 +678,15 @@ __device__ void attention_phase(PP pp, Shared& sh_, int layer, unsigned* err) {
       i16x4 vf[8];
       const uint32_t koff = static_cast<uint32_t>((((kt + col) & (BS - 1)) * kD + 32 * grp) * 2);
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) kf[kk] = __builtin_bit_cast(frag8, dev_load16(rk, koff + kk * 16));
+      for (int kk = 0; kk < 4; ++kk)
+        kf[kk] = __builtin_bit_cast(frag8, p.plain ? __builtin_amdgcn_raw_buffer_load_b128(rk, koff + kk * 16, 0, 0)
+                                                   : dev_load16(rk, koff + kk * 16));
       const uint32_t voff = static_cast<uint32_t>((col * BS + ((kt + 4 * grp) & (BS - 1))) * 2);
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt)
-        vf[dt] = __builtin_bit_cast(i16x4, __builtin_amdgcn_raw_buffer_load_b64(rv, voff + dt * 16 * BS * 2, 0, kScDevice));
+        vf[dt] = __builtin_bit_cast(
+            i16x4, p.plain ? __builtin_amdgcn_raw_buffer_load_b64(rv, voff + dt * 16 * BS * 2, 0, 0)
+                           : __builtin_amdgcn_raw_buffer_load_b64(rv, voff + dt * 16 * BS * 2, 0, kScDevice));
       f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kk], qf[kk], sacc, 0, 0, 0);
@@ -1041,6 +1060,11 @@ int atta_decode_step(const DecodeStepArgs& a, hipStream_t stream) {
       infl * nload > mk::kSlots - 2)
     return -1;
   mk::Params p{};
+  static const int plain = [] {
+    const char* e = std::getenv("ATTA_MK_PLAIN_LOADS");
+    return e ? std::atoi(e) : 0;
+  }();
+  p.plain = plain;
   p.nloaders = nload;
   p.inflight = infl;
   p.M = a.M;

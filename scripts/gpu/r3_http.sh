@@ -14,6 +14,7 @@ for s in $STAGES; do case $s in
   av70) run r3_http_agentverse_70b 700 python bench.py --model llama-3-70b --quantization fp8 --via http --workload agentverse --steps 1 --warmup 1 --max-tokens-limit 128 ;;
   px70) run r3_http_proxy_70b 700 python bench.py --model llama-3-70b --quantization fp8 --via http --workload proxy --steps 1 --warmup 1 --max-tokens-limit 128 ;;
   e70) run r3_llama70b_tp1_fp8 600 python bench.py --model llama-3-70b --quantization fp8 --steps 1 --warmup 1 --verbose ;;
+  e70b) run r3_llama70b_tp1_bf16 700 python bench.py --model llama-3-70b --steps 1 --warmup 1 --verbose ;;
   tp8) rm -rf $OUT/graphs; ATTA_GRAPH_DUMP_DIR=$OUT/graphs run r3_tp8_dump 600 python bench.py --parallel tp --gpus 8 --tp-same-device --model llama-70b-tp-slice --steps 1 --warmup 0 --max-tokens 64 --max-num-seqs 8 --verbose \
        && python scripts/gpu/graph_nodes.py $OUT/graphs > $OUT/r3_tp8_graph_nodes.txt; tail -12 $OUT/r3_tp8_graph_nodes.txt ;;
 esac; done
