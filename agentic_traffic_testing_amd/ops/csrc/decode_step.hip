@@ -81,9 +81,7 @@ struct LayerW {
 struct Params {
   int M, H, I, V, L, NQ, NKV, G;
   int nloaders, inflight;  // loader waves, chunks each keeps in flight
-  int plain;               // EXPERIMENT ONLY (ATTA_MK_PLAIN_LOADS=1): x / q / K / V read through
-                           // the L2 without sc1 - may read stale lines; timing probe of what a
-                           // write-once-buffer design would gain
+  int attn_w;              // attention phase: 1 = one unit per wave (attention_phase_w)
   int bt_stride, bs_shift, max_parts;
   float eps, scale_log2;
   const LayerW* layers;
@@ -447,9 +445,7 @@ __device__ void gemv_phase(PP pp, Shared& sh_, int layer, const XSrc& xs,
         xf[u] = *reinterpret_cast<const frag8*>(xs.erow + k);
       } else {
         const uint32_t off = static_cast<uint32_t>((col * xs.row_stride + k) * 2);
-        xf[u] = __builtin_bit_cast(
-            frag8, p.plain ? __builtin_amdgcn_raw_buffer_load_b128(xs.rs, off, 0, 0)
-                           : dev_load16(xs.rs, off));
+        xf[u] = __builtin_bit_cast(frag8, dev_load16(xs.rs, off));
       }
     }
   };
@@ -662,9 +658,7 @@ __device__ void attention_phase(PP pp, Shared& sh_, int layer, unsigned* err) {
           (static_cast<int64_t>(s) * p.NQ * kD + (hk * G + (ok ? col : 0)) * kD + 32 * grp) * 2);
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk)
-        qf[kk] = ok ? __builtin_bit_cast(frag8, p.plain ? __builtin_amdgcn_raw_buffer_load_b128(rq, off + kk * 16, 0, 0)
-                                                        : dev_load16(rq, off + kk * 16))
-                    : frag8{};
+        qf[kk] = ok ? __builtin_bit_cast(frag8, dev_load16(rq, off + kk * 16)) : frag8{};
     }
     f32x4 o[8];
 #pragma unroll
@@ -678,15 +672,11 @@ __device__ void attention_phase(PP pp, Shared& sh_, int layer, unsigned* err) {
       i16x4 vf[8];
       const uint32_t koff = static_cast<uint32_t>((((kt + col) & (BS - 1)) * kD + 32 * grp) * 2);
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
-        kf[kk] = __builtin_bit_cast(frag8, p.plain ? __builtin_amdgcn_raw_buffer_load_b128(rk, koff + kk * 16, 0, 0)
-                                                   : dev_load16(rk, koff + kk * 16));
+      for (int kk = 0; kk < 4; ++kk) kf[kk] = __builtin_bit_cast(frag8, dev_load16(rk, koff + kk * 16));
       const uint32_t voff = static_cast<uint32_t>((col * BS + ((kt + 4 * grp) & (BS - 1))) * 2);
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt)
-        vf[dt] = __builtin_bit_cast(
-            i16x4, p.plain ? __builtin_amdgcn_raw_buffer_load_b64(rv, voff + dt * 16 * BS * 2, 0, 0)
-                           : __builtin_amdgcn_raw_buffer_load_b64(rv, voff + dt * 16 * BS * 2, 0, kScDevice));
+        vf[dt] = __builtin_bit_cast(i16x4, __builtin_amdgcn_raw_buffer_load_b64(rv, voff + dt * 16 * BS * 2, 0, kScDevice));
       f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kk], qf[kk], sacc, 0, 0, 0);
@@ -849,6 +839,181 @@ __device__ void attention_phase(PP pp, Shared& sh_, int layer, unsigned* err) {
   }
 }
 
+// ---- attention phase, one 128-token unit per WAVE ------------------------------------------
+// The workgroup version above runs one (sequence, kv head, partition) unit at a time with all
+// 8 waves on it, so each unit's dependent chain (q / K / V load -> LDS merge -> partial store
+// ack -> counter atomic -> merge loads) is paid serially, ~4 units per workgroup at B = 5
+// (56 us per layer measured: profiles/r3_megakernel_timeline_L4_F3.txt).  Here every compute
+// wave owns whole units: 8 16-token tiles with an online softmax (next tile's K / V in flight
+// while the current one computes), its partial straight to global memory, the partition
+// counter's last arriver (a wave) merging every partition - no LDS, no workgroup barriers, 8
+// units in flight per workgroup.
+template <int G>
+__device__ void attention_phase_w(PP pp, int layer) {
+  const auto& p = *fresh(pp);
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = lane & 15, grp = lane >> 4;
+  const int P = p.max_parts;
+  const int units = p.M * p.NKV * P;
+  const int BS = 1 << p.bs_shift;
+  const int64_t hs = static_cast<int64_t>(BS) * kD;
+  const uint16_t* kc_l = p.k_cache + layer * p.cache_layer_elems;
+  const uint16_t* vc_l = p.v_cache + layer * p.cache_layer_elems;
+  const auto rq = dev_rsrc(p.q);
+  const auto rpo = dev_rsrc(p.part_out);
+  const auto rpl = dev_rsrc(p.part_lse);
+  const auto ratt = dev_rsrc(p.attn);
+  constexpr float kNegInf = -__builtin_huge_valf();
+  const int nw = p.G * kCW;
+  for (int u = blockIdx.x * kCW + w; u < units; u += nw) {
+    const int s = u / (p.NKV * P);
+    const int hk = (u / P) % p.NKV;
+    const int part = u % P;
+    const int kvlen = p.seq_kvlen[s];
+    const int nparts = (kvlen + kPartTokens - 1) / kPartTokens;
+    if (part >= nparts) continue;  // wave-uniform
+    const int kv_begin = part * kPartTokens;
+    const int kv_end = min(kvlen, kv_begin + kPartTokens);
+    const int ntile = (kv_end - kv_begin + 15) >> 4;
+    frag8 qf[4];
+    {
+      const bool ok = col < G;
+      const uint32_t off = static_cast<uint32_t>(
+          (static_cast<int64_t>(s) * p.NQ * kD + (hk * G + (ok ? col : 0)) * kD + 32 * grp) * 2);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+        qf[kk] = ok ? __builtin_bit_cast(frag8, dev_load16(rq, off + kk * 16)) : frag8{};
+    }
+    auto load_kv = [&](int t, frag8 (&kf)[4], i16x4 (&vf)[8]) {
+      const int kt = kv_begin + 16 * t;
+      const int page = p.block_tables[static_cast<int64_t>(s) * p.bt_stride + (kt >> p.bs_shift)];
+      const auto rk = dev_rsrc(kc_l + (static_cast<int64_t>(page) * p.NKV + hk) * hs);
+      const auto rv = dev_rsrc(vc_l + (static_cast<int64_t>(page) * p.NKV + hk) * hs);
+      const uint32_t koff = static_cast<uint32_t>((((kt + col) & (BS - 1)) * kD + 32 * grp) * 2);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) kf[kk] = __builtin_bit_cast(frag8, dev_load16(rk, koff + kk * 16));
+      const uint32_t voff = static_cast<uint32_t>((col * BS + ((kt + 4 * grp) & (BS - 1))) * 2);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+        vf[dt] = __builtin_bit_cast(i16x4, __builtin_amdgcn_raw_buffer_load_b64(rv, voff + dt * 16 * BS * 2, 0, kScDevice));
+    };
+    f32x4 o[8];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m_run = kNegInf, l_run = 0.f;
+    frag8 ka[4], kb[4];
+    i16x4 va[8], vb[8];
+    auto tile = [&](int t, const frag8 (&kf)[4], const i16x4 (&vf)[8]) {
+      const int kt = kv_begin + 16 * t;
+      f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kk], qf[kk], sacc, 0, 0, 0);
+      float sv[4], tmax = kNegInf;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sv[j] = (kt + 4 * grp + j < kv_end) ? sacc[j] * p.scale_log2 : kNegInf;
+        tmax = fmaxf(tmax, sv[j]);
+      }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, kWave));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, kWave));
+      const float m_new = fmaxf(m_run, tmax);
+      const float m_use = (m_new == kNegInf) ? 0.f : m_new;
+      const float corr = exp2f(m_run - m_use);  // 0 on the first tile (m_run = -inf)
+      float psum = 0.f;
+      i16x4 pf;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float pv = exp2f(sv[j] - m_use);
+        psum += pv;
+        pf[j] = static_cast<short>(tobf(pv));
+      }
+      psum += __shfl_xor(psum, 16, kWave);
+      psum += __shfl_xor(psum, 32, kWave);
+      l_run = l_run * corr + psum;
+      m_run = m_new;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        o[dt] *= corr;
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vf[dt], pf, o[dt], 0, 0, 0);
+      }
+    };
+    load_kv(0, ka, va);
+    for (int t = 0; t < ntile; t += 2) {
+      if (t + 1 < ntile) load_kv(t + 1, kb, vb);
+      tile(t, ka, va);
+      if (t + 1 >= ntile) break;
+      if (t + 2 < ntile) load_kv(t + 2, ka, va);
+      tile(t + 1, kb, vb);
+    }
+    // lane holds o[dt][j] = dims 16 dt + 4 grp + j of head column col
+    const float invL = l_run > 0.f ? 1.f / l_run : 0.f;
+    if (nparts == 1) {
+      if (col < G) {
+        const uint32_t base = static_cast<uint32_t>(
+            (static_cast<int64_t>(s) * p.NQ * kD + (hk * G + col) * kD + 4 * grp) * 2);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+          const uint32_t lo = static_cast<uint32_t>(tobf(o[dt][0] * invL)) | (static_cast<uint32_t>(tobf(o[dt][1] * invL)) << 16);
+          const uint32_t hi = static_cast<uint32_t>(tobf(o[dt][2] * invL)) | (static_cast<uint32_t>(tobf(o[dt][3] * invL)) << 16);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned,
+                                                                   (__attribute__((ext_vector_type(2))) unsigned){lo, hi}),
+                                                ratt, base + dt * 32, 0, kScDevice);
+        }
+      }
+      continue;
+    }
+    const int64_t shk = static_cast<int64_t>(s) * p.NKV + hk;
+    if (col < G) {
+      const int64_t pbase = (shk * P + part) * 16 + col;
+      const uint32_t off = static_cast<uint32_t>((pbase * kD + 4 * grp) * 4);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+        dev_store16(rpo, off + dt * 64, __builtin_bit_cast(u32x4, o[dt] * invL));
+      if (grp == 0)
+        dev_store4(rpl, static_cast<uint32_t>(pbase * 4), (l_run > 0.f) ? (m_run + log2f(l_run)) : kNegInf);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int old = 0;
+    if (lane == 0)
+      old = __hip_atomic_fetch_add(p.att_counters + shk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __shfl(old, 0, kWave);
+    if (old != nparts - 1) continue;
+    // ---- last arriving wave: merge every partition of (s, hk) in partition order ------------
+    // lane -> head column mc = lane >> 4 (< G), 8 dims md0 = (lane & 15) * 8
+    const int mc = lane >> 4, md0 = (lane & 15) * 8;
+    if (mc < G) {
+      float mr = kNegInf, wsum = 0.f;
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < nparts; ++q) {
+        const int64_t pbase = (shk * P + q) * 16 + mc;
+        const float lse = dev_load4(rpl, static_cast<uint32_t>(pbase * 4));
+        const uint32_t off = static_cast<uint32_t>((pbase * kD + md0) * 4);
+        const f32x4 pa = __builtin_bit_cast(f32x4, dev_load16(rpo, off));
+        const f32x4 pb = __builtin_bit_cast(f32x4, dev_load16(rpo, off + 16));
+        if (lse == kNegInf) continue;
+        const float m_new = fmaxf(mr, lse);
+        const float sc = exp2f(mr - m_new);
+        const float wt = exp2f(lse - m_new);
+        wsum = wsum * sc + wt;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          acc[jj] = acc[jj] * sc + wt * pa[jj];
+          acc[4 + jj] = acc[4 + jj] * sc + wt * pb[jj];
+        }
+        mr = m_new;
+      }
+      const float inv = wsum > 0.f ? 1.f / wsum : 0.f;
+      u32x4 o8;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        o8[j] = static_cast<uint32_t>(tobf(acc[2 * j] * inv)) | (static_cast<uint32_t>(tobf(acc[2 * j + 1] * inv)) << 16);
+      dev_store16(ratt, static_cast<uint32_t>((static_cast<int64_t>(s) * p.NQ * kD + (hk * G + mc) * kD + md0) * 2), o8);
+    }
+    if (lane == 0) __hip_atomic_store(p.att_counters + shk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // ---- the kernel ------------------------------------------------------------------------------
 template <int G>
 __global__ void __launch_bounds__(kThreads, 1) decode_step_kernel(const Params* __restrict__ gp) {
@@ -914,7 +1079,10 @@ __global__ void __launch_bounds__(kThreads, 1) decode_step_kernel(const Params* 
     if (wave == 0) poll_phase(p, base + K_QKV, err);
     cbar(sh, err);
     if (wave == 0 && ((base + 1) % p.G) == static_cast<int>(blockIdx.x) && base - 1 >= 1) zero_phase(p, base - 1);
-    attention_phase<G>(pp, sh, l, err);
+    if (p.attn_w)
+      attention_phase_w<G>(pp, l);
+    else
+      attention_phase<G>(pp, sh, l, err);
     arrive_phase(p, sh, base + K_ATT, err);
     // O(l)
     if (wave == 0) poll_phase(p, base + K_ATT, err);
@@ -1060,11 +1228,14 @@ int atta_decode_step(const DecodeStepArgs& a, hipStream_t stream) {
       infl * nload > mk::kSlots - 2)
     return -1;
   mk::Params p{};
-  static const int plain = [] {
-    const char* e = std::getenv("ATTA_MK_PLAIN_LOADS");
-    return e ? std::atoi(e) : 0;
+  // attention phase: per-wave units win at B = 5 (47.9 vs 57.7 us per layer), the
+  // workgroup version at B = 1 (20.0 vs 44.9 us; its merge is spread over 8 waves):
+  // profiles/r3_megakernel_timeline_attnw*.txt.  ATTA_MK_ATTN_WAVE=0/1 forces one.
+  static const int attn_w = [] {
+    const char* e = std::getenv("ATTA_MK_ATTN_WAVE");
+    return e ? std::atoi(e) : -1;
   }();
-  p.plain = plain;
+  p.attn_w = attn_w >= 0 ? attn_w : (a.M >= 4 ? 1 : 0);
   p.nloaders = nload;
   p.inflight = infl;
   p.M = a.M;

@@ -5,6 +5,6 @@ export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 OUT=gpurun_out; mkdir -p $OUT
 run() { local name=$1 t=$2; shift 2; echo "=== $name"; timeout -k 10 $t "$@" > $OUT/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; tail -${TAILN:-8} $OUT/$name.log; if [ $rc -ne 0 ]; then echo STOP; exit $rc; fi; }
 TAILN=4 run r3_mk_tests4 400 python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests/test_engine.py -k "megakernel"
-for pl in 0 1; do
-  ATTA_MK_PLAIN_LOADS=$pl TAILN=22 run r3_mk_prof_plain$pl 300 python scripts/gpu/mk_profile.py --steps 24 --rows 1 5
+for aw in 1 0; do
+  ATTA_MK_ATTN_WAVE=$aw TAILN=22 run r3_mk_prof_attnw$aw 300 python scripts/gpu/mk_profile.py --steps 24 --rows 1 5
 done
