@@ -54,6 +54,9 @@
 namespace atta {
 namespace mk {
 
+// cache policy of the activation / q / K / V loads: sc1 (device scope, L2 bypass) - what makes
+// reading another XCD's same-launch writes correct
+constexpr int kXAux = kScDevice;
 constexpr int kCW = 8;                    // compute waves
 constexpr int kMaxLoaders = 4;
 constexpr int kThreads = (kCW + kMaxLoaders) * 64;  // + up to 4 loader waves
@@ -445,7 +448,7 @@ __device__ void gemv_phase(PP pp, Shared& sh_, int layer, const XSrc& xs,
         xf[u] = *reinterpret_cast<const frag8*>(xs.erow + k);
       } else {
         const uint32_t off = static_cast<uint32_t>((col * xs.row_stride + k) * 2);
-        xf[u] = __builtin_bit_cast(frag8, dev_load16(xs.rs, off));
+        xf[u] = __builtin_bit_cast(frag8, __builtin_amdgcn_raw_buffer_load_b128(xs.rs, off, 0, kXAux));
       }
     }
   };
@@ -658,7 +661,7 @@ __device__ void attention_phase(PP pp, Shared& sh_, int layer, unsigned* err) {
           (static_cast<int64_t>(s) * p.NQ * kD + (hk * G + (ok ? col : 0)) * kD + 32 * grp) * 2);
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk)
-        qf[kk] = ok ? __builtin_bit_cast(frag8, dev_load16(rq, off + kk * 16)) : frag8{};
+        qf[kk] = ok ? __builtin_bit_cast(frag8, __builtin_amdgcn_raw_buffer_load_b128(rq, off + kk * 16, 0, kXAux)) : frag8{};
     }
     f32x4 o[8];
 #pragma unroll
@@ -672,11 +675,11 @@ __device__ void attention_phase(PP pp, Shared& sh_, int layer, unsigned* err) {
       i16x4 vf[8];
       const uint32_t koff = static_cast<uint32_t>((((kt + col) & (BS - 1)) * kD + 32 * grp) * 2);
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) kf[kk] = __builtin_bit_cast(frag8, dev_load16(rk, koff + kk * 16));
+      for (int kk = 0; kk < 4; ++kk) kf[kk] = __builtin_bit_cast(frag8, __builtin_amdgcn_raw_buffer_load_b128(rk, koff + kk * 16, 0, kXAux));
       const uint32_t voff = static_cast<uint32_t>((col * BS + ((kt + 4 * grp) & (BS - 1))) * 2);
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt)
-        vf[dt] = __builtin_bit_cast(i16x4, __builtin_amdgcn_raw_buffer_load_b64(rv, voff + dt * 16 * BS * 2, 0, kScDevice));
+        vf[dt] = __builtin_bit_cast(i16x4, __builtin_amdgcn_raw_buffer_load_b64(rv, voff + dt * 16 * BS * 2, 0, kXAux));
       f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kk], qf[kk], sacc, 0, 0, 0);
@@ -883,7 +886,7 @@ __device__ void attention_phase_w(PP pp, int layer) {
           (static_cast<int64_t>(s) * p.NQ * kD + (hk * G + (ok ? col : 0)) * kD + 32 * grp) * 2);
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk)
-        qf[kk] = ok ? __builtin_bit_cast(frag8, dev_load16(rq, off + kk * 16)) : frag8{};
+        qf[kk] = ok ? __builtin_bit_cast(frag8, __builtin_amdgcn_raw_buffer_load_b128(rq, off + kk * 16, 0, kXAux)) : frag8{};
     }
     auto load_kv = [&](int t, frag8 (&kf)[4], i16x4 (&vf)[8]) {
       const int kt = kv_begin + 16 * t;
@@ -892,11 +895,11 @@ __device__ void attention_phase_w(PP pp, int layer) {
       const auto rv = dev_rsrc(vc_l + (static_cast<int64_t>(page) * p.NKV + hk) * hs);
       const uint32_t koff = static_cast<uint32_t>((((kt + col) & (BS - 1)) * kD + 32 * grp) * 2);
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) kf[kk] = __builtin_bit_cast(frag8, dev_load16(rk, koff + kk * 16));
+      for (int kk = 0; kk < 4; ++kk) kf[kk] = __builtin_bit_cast(frag8, __builtin_amdgcn_raw_buffer_load_b128(rk, koff + kk * 16, 0, kXAux));
       const uint32_t voff = static_cast<uint32_t>((col * BS + ((kt + 4 * grp) & (BS - 1))) * 2);
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt)
-        vf[dt] = __builtin_bit_cast(i16x4, __builtin_amdgcn_raw_buffer_load_b64(rv, voff + dt * 16 * BS * 2, 0, kScDevice));
+        vf[dt] = __builtin_bit_cast(i16x4, __builtin_amdgcn_raw_buffer_load_b64(rv, voff + dt * 16 * BS * 2, 0, kXAux));
     };
     f32x4 o[8];
 #pragma unroll
