@@ -318,7 +318,7 @@ __device__ __forceinline__ void wait_chunks_in_flight(int f) {
 // ~128 KiB in flight: one wave's vmcnt window (<= 7 chunks) cannot hold that, several
 // loader waves can).  Deadlock-free while inflight * nloaders < kSlots - 1: publishing chunk
 // n then only needs slots freed by chunks < n.
-__device__ void loader(PP pp, Shared& sh, unsigned* err, int r) {
+__device__ __forceinline__ void loader(PP pp, Shared& sh, unsigned* err, int r) {
   const auto& p = *pp;
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.x;
@@ -386,6 +386,57 @@ __device__ void loader(PP pp, Shared& sh, unsigned* err, int r) {
   }
 }
 
+// ---- register-streaming mode (no loader waves): every compute wave streams its own chunks ----
+// The loader-ring mode above couples all 8 compute waves to 4 loader waves through 16 shared
+// slots: a compute wave that is late (x load, epilogue, barrier) holds its slots and stalls
+// every loader (measured: loaders wait on FREE slots 52-60 % of the time,
+// profiles/r3_megakernel_timeline_*.txt), and 12 waves per CU cap a wave at 168 VGPRs.  In
+// streaming mode (ATTA_MK_LOADERS=0) each of the 8 compute waves DMAs the weight chunks it
+// will itself consume (its K slice of every tile of every phase, in stream order) into two
+// private 8 KB LDS slots, two chunks ahead: no cross-wave hand-off, 256 VGPRs per wave, and
+// the first two chunks of the next phase go out right after a phase's arrive, so they are in
+// flight during the grid barrier.
+struct Stream {
+  int sp, i, j;        // cursor: next chunk to issue (stream phase, tile index, chunk index)
+  unsigned issued, consumed;
+};
+
+template <typename P>
+__device__ __forceinline__ void stream_skip_empty(const P& p, Stream& st) {
+  while (st.sp <= 4 * p.L &&
+         tiles_of(stream_phase(p, st.sp).ntiles, static_cast<int>(blockIdx.x), p.G) == 0)
+    ++st.sp;
+}
+
+template <typename P>
+__device__ __forceinline__ void stream_issue(const P& p, Shared& sh, Stream& st, int w) {
+  const int lane = threadIdx.x & 63;
+  const StreamPhase ph = stream_phase(p, st.sp);
+  const int nb = ph.K / 256;
+  const int tile = static_cast<int>(blockIdx.x) + st.i * p.G;
+  const uint16_t* src = ph.w + (static_cast<int64_t>(tile) * (ph.K / 32) + w * nb + st.j * 8) * 512 + lane * 8;
+  const uint32_t ring0 = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sh.ring)));
+  const uint32_t dst = ring0 + static_cast<uint32_t>((2 * w + (st.issued & 1)) * kSlotBytes);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) dma16(src + u * 512, __builtin_amdgcn_readfirstlane(dst + u * 1024));
+  ++st.issued;
+  if (++st.j == nb / 8) {
+    st.j = 0;
+    if (++st.i == tiles_of(ph.ntiles, static_cast<int>(blockIdx.x), p.G)) {
+      st.i = 0;
+      ++st.sp;
+      stream_skip_empty(p, st);
+    }
+  }
+}
+
+// keep two chunks in flight (issue across phase boundaries: weights never depend on activations)
+template <typename P>
+__device__ __forceinline__ void stream_top_up(const P& p, Shared& sh, Stream& st, int w) {
+  while (st.issued - st.consumed < 2 && st.sp <= 4 * p.L) stream_issue(p, sh, st, w);
+}
+
 // ---- compute-wave GEMV phase ----------------------------------------------------------------
 typedef bf16x8 frag8;
 
@@ -421,7 +472,7 @@ struct XSrc {  // where the A operand (activation rows) of a GEMV phase comes fr
 };
 
 template <int KIND>
-__device__ void gemv_phase(PP pp, Shared& sh_, int layer, const XSrc& xs,
+__device__ __forceinline__ void gemv_phase(PP pp, Shared& sh_, int layer, const XSrc& xs,
                            uint32_t& seq, unsigned* err) {
   const auto& p = *fresh(pp);
   Shared& sh = fresh_lds(sh_);
@@ -623,9 +674,223 @@ __device__ void gemv_phase(PP pp, Shared& sh_, int layer, const XSrc& xs,
   }
 }
 
+template <int KIND>
+__device__ __forceinline__ void gemv_phase_rs(PP pp, Shared& sh_, int layer, const XSrc& xs, Stream& st,
+                              unsigned* err) {
+  const auto& p = *fresh(pp);
+  Shared& sh = fresh_lds(sh_);
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = lane & 15, grp = lane >> 4;
+  const int c = blockIdx.x;
+  const int sp = KIND == 5 ? 4 * p.L : 4 * layer + (KIND == K_QKV ? 0 : KIND == K_O ? 1 : KIND == K_GU ? 2 : 3);
+  const StreamPhase ph = stream_phase(p, sp);
+  const int nt = tiles_of(ph.ntiles, c, p.G);
+  const int nb = ph.K / 256;
+  const int nch = nb / 8;
+  constexpr bool norm = (KIND == K_QKV || KIND == K_GU || KIND == 5);
+  const bool rowok = col < p.M;
+  const int kw0 = w * nb * 32;  // first k of this wave's slice
+  // x fragment loads of chunk j (this lane: row col, k-group grp)
+  auto load_x = [&](frag8 (&xf)[8], int j) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = kw0 + j * 256 + u * 32 + 8 * grp;
+      if (!rowok) {
+        xf[u] = frag8{};
+      } else if (xs.embed) {
+        xf[u] = *reinterpret_cast<const frag8*>(xs.erow + k);
+      } else {
+        const uint32_t off = static_cast<uint32_t>((col * xs.row_stride + k) * 2);
+        xf[u] = __builtin_bit_cast(frag8, __builtin_amdgcn_raw_buffer_load_b128(xs.rs, off, 0, kXAux));
+      }
+    }
+  };
+  // x: nch <= 2 (K = 4096) -> the wave's whole K slice loaded once per phase; otherwise the
+  // next chunk's x is prefetched (issued before the chunk's weight DMA, so the counted wait
+  // below covers both)
+  const bool keep = nch <= 2;
+  frag8 x0[8], x1[8];
+  load_x(x0, 0);
+  if (keep && nch > 1) load_x(x1, 1);
+  for (int i = 0; i < nt; ++i) {
+    const int tile = c + i * p.G;
+    const int tb = i & 1;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    float ss = 0.f;
+    auto chunk = [&](const frag8 (&xa)[8], int j) __attribute__((always_inline)) {
+      // this chunk's DMA landed: keep only the newer chunk (8 DMAs) in flight
+      if (st.issued - st.consumed >= 2)
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      const uint8_t* sb = sh.ring + (2 * w + (st.consumed & 1)) * kSlotBytes + lane * 16;
+      frag8 wf[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) wf[u] = *reinterpret_cast<const frag8*>(sb + u * 1024);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      ++st.consumed;
+      if (!keep) {  // next chunk's x (the next tile's first after the last)
+        if (j + 1 < nch)
+          load_x(x1, j + 1);
+        else if (i + 1 < nt)
+          load_x(x1, 0);
+      }
+      // refill the freed slot - only with this phase's chunks (the next phase's go out after
+      // the arrive, so its vmcnt(0) drains the epilogue stores, not prefetches)
+      if (st.sp == sp) stream_issue(p, sh, st, w);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[u], wf[u], acc, 0, 0, 0);
+        if (norm && i == 0) ss = sq8(xa[u], ss);
+      }
+    };
+    if (keep) {
+      chunk(x0, 0);
+      if (nch > 1) chunk(x1, 1);
+    } else {
+      for (int j = 0; j < nch; ++j) {
+        chunk(x0, j);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x0[u] = x1[u];
+      }
+    }
+    // ---- cross-wave reduction ----------------------------------------------------------
+    Red& r = sh.s.red;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = 4 * grp + e;
+      if (m < p.M) r.acc[tb][w][m][col] = acc[e];
+    }
+    if (norm && i == 0) {
+      ss += __shfl_xor(ss, 16, kWave);
+      ss += __shfl_xor(ss, 32, kWave);
+      if (grp == 0 && rowok) r.ss[0][w][col] = ss;
+    }
+    cbar(sh, err);
+    // ---- epilogue (threads e < outputs of the tile) ----------------------------------------
+    const int e = threadIdx.x;
+    auto inv_rms = [&](int m) {
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < kCW; ++q) s += r.ss[0][q][m];
+      return rsqrtf(s / static_cast<float>(ph.K) + p.eps);
+    };
+    auto red_sum = [&](int m, int n) {
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < kCW; ++q) s += r.acc[tb][q][m][n];
+      return s;
+    };
+    if constexpr (KIND == K_O || KIND == K_DOWN) {
+      // residual += acc: thread e -> row e >> 3, columns 2 (e & 7) .. +1 (4-byte sc1 access)
+      if (e < p.M * 8) {
+        const int m = e >> 3, n = 2 * (e & 7);
+        const auto rx = dev_rsrc(p.x);
+        const uint32_t off = static_cast<uint32_t>((static_cast<int64_t>(m) * p.H + tile * 16 + n) * 2);
+        const uint32_t old = __builtin_amdgcn_raw_buffer_load_b32(rx, off, 0, kScDevice);
+        const float v0 = bf(tobf(red_sum(m, n))) + bf(static_cast<uint16_t>(old & 0xffff));
+        const float v1 = bf(tobf(red_sum(m, n + 1))) + bf(static_cast<uint16_t>(old >> 16));
+        const uint32_t nv = static_cast<uint32_t>(tobf(v0)) | (static_cast<uint32_t>(tobf(v1)) << 16);
+        __builtin_amdgcn_raw_buffer_store_b32(nv, rx, off, 0, kScDevice);
+      }
+    } else if constexpr (KIND == K_GU) {
+      // silu(gate_j) * up_j for j = 2 (e & 3) .. +1 of row e >> 2 (tile covers act 8 t .. +7)
+      if (e < p.M * 4) {
+        const int m = e >> 2, j = 2 * (e & 3);
+        const float sc = inv_rms(m);
+        float o[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float g = bf(tobf(red_sum(m, j + h) * sc));
+          const float u = bf(tobf(red_sum(m, j + h + 8) * sc));
+          const float si = bf(tobf(g / (1.f + __expf(-g))));
+          o[h] = si * u;
+        }
+        const uint32_t nv = static_cast<uint32_t>(tobf(o[0])) | (static_cast<uint32_t>(tobf(o[1])) << 16);
+        const uint32_t off = static_cast<uint32_t>((static_cast<int64_t>(m) * p.I + tile * 8 + j) * 2);
+        __builtin_amdgcn_raw_buffer_store_b32(nv, dev_rsrc(p.act), off, 0, kScDevice);
+      }
+    } else if constexpr (KIND == K_QKV) {
+      // RoPE pairs (d, d + 64): tile = head * 8 + jj covers d = 8 jj .. +7 (cols 0-7) and
+      // d + 64 (cols 8-15); thread e -> row e >> 2, d pair 2 (e & 3) .. +1
+      if (e < p.M * 4) {
+        const int m = e >> 2, cc = 2 * (e & 3);
+        const int head = tile >> 3, d0 = (tile & 7) * 8 + cc;
+        const float sc = inv_rms(m);
+        const int nq = p.NQ, nkv = p.NKV;
+        const int slot = p.slots[m];
+        float o1[2], o2[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float x1 = bf(tobf(red_sum(m, cc + h) * sc));
+          const float x2 = bf(tobf(red_sum(m, cc + h + 8) * sc));
+          if (head < nq + nkv) {
+            const float* cs = p.cos_sin + static_cast<int64_t>(p.positions[m]) * 128;
+            const float co = cs[d0 + h], si = cs[64 + d0 + h];
+            o1[h] = x1 * co - x2 * si;
+            o2[h] = x2 * co + x1 * si;
+          } else {
+            o1[h] = x1;
+            o2[h] = x2;
+          }
+        }
+        const uint32_t lo = static_cast<uint32_t>(tobf(o1[0])) | (static_cast<uint32_t>(tobf(o1[1])) << 16);
+        const uint32_t hi = static_cast<uint32_t>(tobf(o2[0])) | (static_cast<uint32_t>(tobf(o2[1])) << 16);
+        const int BS = 1 << p.bs_shift;
+        if (head < nq) {
+          const auto rq = dev_rsrc(p.q);
+          const uint32_t off = static_cast<uint32_t>((static_cast<int64_t>(m) * nq * kD + head * kD + d0) * 2);
+          __builtin_amdgcn_raw_buffer_store_b32(lo, rq, off, 0, kScDevice);
+          __builtin_amdgcn_raw_buffer_store_b32(hi, rq, off + 128, 0, kScDevice);
+        } else if (slot >= 0 && head < nq + nkv) {
+          const int hk = head - nq;
+          uint16_t* kc = p.k_cache + layer * p.cache_layer_elems +
+                         ((static_cast<int64_t>(slot >> p.bs_shift) * nkv + hk) * BS + (slot & (BS - 1))) * kD;
+          // per-row cache addresses: device-scope (sc1) global stores, no per-thread rsrc
+          __hip_atomic_store(reinterpret_cast<uint32_t*>(kc + d0), lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(reinterpret_cast<uint32_t*>(kc + d0 + 64), hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (slot >= 0) {
+          const int hk = head - nq - nkv;
+          uint16_t* vc = p.v_cache + layer * p.cache_layer_elems +
+                         (static_cast<int64_t>(slot >> p.bs_shift) * nkv + hk) * kD * BS + (slot & (BS - 1));
+          __hip_atomic_store(vc + d0 * BS, static_cast<uint16_t>(lo & 0xffff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(vc + (d0 + 1) * BS, static_cast<uint16_t>(lo >> 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(vc + (d0 + 64) * BS, static_cast<uint16_t>(hi & 0xffff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(vc + (d0 + 65) * BS, static_cast<uint16_t>(hi >> 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    } else {  // LM head: Gumbel-max key of the tile's 16 vocab ids per row
+      if (e < p.M * 16) {
+        const int m = e >> 4, n = e & 15;
+        float v = bf(tobf(red_sum(m, n) * inv_rms(m)));
+        const float t = p.temperature[m];
+        const int idx = tile * 16 + n;
+        if (t > 1e-5f)
+          v = v / t + gumbel(static_cast<uint64_t>(p.seeds[m]), static_cast<uint64_t>(p.steps[m]),
+                             static_cast<uint32_t>(idx));
+        unsigned long long key = (static_cast<unsigned long long>(ordered_bits(v)) << 32) |
+                                 static_cast<unsigned long long>(0xFFFFFFFFu - static_cast<unsigned>(idx));
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          const unsigned long long other = __shfl_xor(key, o, kWave);
+          key = other > key ? other : key;
+        }
+        if (n == 0) {
+          const uint32_t off = static_cast<uint32_t>((static_cast<int64_t>(m) * (p.V / 16) + tile) * 8);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, key),
+                                                dev_rsrc(p.keys), off, 0, kScDevice);
+        }
+      }
+    }
+  }
+}
+
 // ---- attention phase ---------------------------------------------------------------------
 template <int G>
-__device__ void attention_phase(PP pp, Shared& sh_, int layer, unsigned* err) {
+__device__ __forceinline__ void attention_phase(PP pp, Shared& sh_, int layer, unsigned* err) {
   const auto& p = *fresh(pp);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -852,7 +1117,7 @@ __device__ void attention_phase(PP pp, Shared& sh_, int layer, unsigned* err) {
 // counter's last arriver (a wave) merging every partition - no LDS, no workgroup barriers, 8
 // units in flight per workgroup.
 template <int G>
-__device__ void attention_phase_w(PP pp, int layer) {
+__device__ __forceinline__ void attention_phase_w(PP pp, int layer) {
   const auto& p = *fresh(pp);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1018,8 +1283,8 @@ __device__ void attention_phase_w(PP pp, int layer) {
 }
 
 // ---- the kernel ------------------------------------------------------------------------------
-template <int G>
-__global__ void __launch_bounds__(kThreads, 1) decode_step_kernel(const Params* __restrict__ gp) {
+template <int G, bool RS>
+__global__ void __launch_bounds__(RS ? kCW * 64 : kThreads, 1) decode_step_kernel(const Params* __restrict__ gp) {
   // the parameter block lives in device memory (a by-value aggregate whose address is taken
   // is copied to scratch); each phase re-reads it through fresh()
   __shared__ Shared sh;
@@ -1041,9 +1306,15 @@ __global__ void __launch_bounds__(kThreads, 1) decode_step_kernel(const Params* 
     if (p.stats != nullptr) p.stats[blockIdx.x * 4 + 3] = 0;
   }
   __syncthreads();  // the only s_barrier: before the roles split
-  if (wave >= kCW) {
+  if (!RS && wave >= kCW) {
     loader(pp, sh, err, wave - kCW);
     return;
+  }
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  Stream st{0, 0, 0, 0u, 0u};
+  if constexpr (RS) {
+    stream_skip_empty(p, st);
+    stream_top_up(p, sh, st, wv);
   }
   // row ids (token of each row: the previous step's device sample under look-ahead)
   const int row = lane & 15;
@@ -1073,11 +1344,16 @@ __global__ void __launch_bounds__(kThreads, 1) decode_step_kernel(const Params* 
     }
     if (l == 0) {
       XSrc xe{dev_rsrc(p.x), p.H, true, p.embed + id * p.H};
-      gemv_phase<K_QKV>(pp, sh, l, xe, seq, err);
+      if constexpr (RS) gemv_phase_rs<K_QKV>(pp, sh, l, xe, st, err);
+      else gemv_phase<K_QKV>(pp, sh, l, xe, seq, err);
     } else {
-      gemv_phase<K_QKV>(pp, sh, l, xres, seq, err);
+      if constexpr (RS) gemv_phase_rs<K_QKV>(pp, sh, l, xres, st, err);
+      else gemv_phase<K_QKV>(pp, sh, l, xres, seq, err);
     }
     arrive_phase(p, sh, base + K_QKV, err);
+    // o_proj's first chunks go out now: they land in LDS while the attention runs (its
+    // vmcnt(0) waits may cover them - they are in flight for the same ~us anyway)
+    if constexpr (RS) stream_top_up(p, sh, st, wv);
     // ATT(l)
     if (wave == 0) poll_phase(p, base + K_QKV, err);
     cbar(sh, err);
@@ -1093,31 +1369,38 @@ __global__ void __launch_bounds__(kThreads, 1) decode_step_kernel(const Params* 
     if (wave == 0 && ((base + 2) % p.G) == static_cast<int>(blockIdx.x)) zero_phase(p, base);
     {
       XSrc xa{dev_rsrc(p.attn), static_cast<int64_t>(p.NQ) * kD, false, nullptr};
-      gemv_phase<K_O>(pp, sh, l, xa, seq, err);
+      if constexpr (RS) gemv_phase_rs<K_O>(pp, sh, l, xa, st, err);
+      else gemv_phase<K_O>(pp, sh, l, xa, seq, err);
     }
     arrive_phase(p, sh, base + K_O, err);
+    if constexpr (RS) stream_top_up(p, sh, st, wv);
     // GU(l)
     if (wave == 0) poll_phase(p, base + K_O, err);
     cbar(sh, err);
     if (wave == 0 && ((base + 3) % p.G) == static_cast<int>(blockIdx.x)) zero_phase(p, base + 1);
-    gemv_phase<K_GU>(pp, sh, l, xres, seq, err);
+    if constexpr (RS) gemv_phase_rs<K_GU>(pp, sh, l, xres, st, err);
+    else gemv_phase<K_GU>(pp, sh, l, xres, seq, err);
     arrive_phase(p, sh, base + K_GU, err);
+    if constexpr (RS) stream_top_up(p, sh, st, wv);
     // DOWN(l)
     if (wave == 0) poll_phase(p, base + K_GU, err);
     cbar(sh, err);
     if (wave == 0 && ((base + 4) % p.G) == static_cast<int>(blockIdx.x)) zero_phase(p, base + 2);
     {
       XSrc xd{dev_rsrc(p.act), p.I, false, nullptr};
-      gemv_phase<K_DOWN>(pp, sh, l, xd, seq, err);
+      if constexpr (RS) gemv_phase_rs<K_DOWN>(pp, sh, l, xd, st, err);
+      else gemv_phase<K_DOWN>(pp, sh, l, xd, seq, err);
     }
     arrive_phase(p, sh, base + K_DOWN, err);
+    if constexpr (RS) stream_top_up(p, sh, st, wv);
   }
   // LM head + sampler keys
   const int lm = 1 + 5 * L;
   if (wave == 0) poll_phase(p, lm - 1, err);
   cbar(sh, err);
   if (wave == 0 && (lm % p.G) == static_cast<int>(blockIdx.x)) zero_phase(p, lm - 2);
-  gemv_phase<5>(pp, sh, 0, xres, seq, err);
+  if constexpr (RS) gemv_phase_rs<5>(pp, sh, 0, xres, st, err);
+  else gemv_phase<5>(pp, sh, 0, xres, seq, err);
   arrive_phase(p, sh, lm, err);
   // FIN: workgroup m < M reduces row m's tile keys to its token
   if (static_cast<int>(blockIdx.x) < p.M) {
@@ -1220,14 +1503,17 @@ int atta_decode_step(const DecodeStepArgs& a, hipStream_t stream) {
   const int grid = atta_decode_step_grid();
   if (grid <= 0) return -1;
   static const int nload = [] {
-    const char* e = std::getenv("ATTA_MK_LOADERS");  // 4 x 3 measured best of 1x7, 2x7, 4x3
-    return e ? std::atoi(e) : 4;                      // (profiles/r3_megakernel_timeline_*)
+    // 0 = register-streaming mode (compute waves DMA their own chunks): 3.41 ms per B = 1 step
+    // vs 4.07 ms for the best loader-ring setting, 4 loaders x 3 chunks
+    // (profiles/r3_megakernel_timeline_rs.txt, r3_megakernel_timeline_L4_F3.txt)
+    const char* e = std::getenv("ATTA_MK_LOADERS");
+    return e ? std::atoi(e) : 0;
   }();
   static const int infl = [] {
     const char* e = std::getenv("ATTA_MK_INFLIGHT");
     return e ? std::atoi(e) : 3;
   }();
-  if (nload < 1 || nload > mk::kMaxLoaders || infl < 1 || infl > 7 ||
+  if (nload < 0 || nload > mk::kMaxLoaders || infl < 1 || infl > 7 ||
       infl * nload > mk::kSlots - 2)
     return -1;
   mk::Params p{};
@@ -1286,10 +1572,18 @@ int atta_decode_step(const DecodeStepArgs& a, hipStream_t stream) {
   const mk::Params* dp = mk::device_params(p, stream);
   if (dp == nullptr) return -3;  // first use of this parameter block while capturing
   const int threads = (mk::kCW + nload) * 64;
-  switch (G) {
-    case 1: mk::decode_step_kernel<1><<<grid, threads, 0, stream>>>(dp); break;
-    case 2: mk::decode_step_kernel<2><<<grid, threads, 0, stream>>>(dp); break;
-    default: mk::decode_step_kernel<4><<<grid, threads, 0, stream>>>(dp); break;
+  if (nload == 0) {  // register-streaming mode: compute waves stream their own chunks
+    switch (G) {
+      case 1: mk::decode_step_kernel<1, true><<<grid, threads, 0, stream>>>(dp); break;
+      case 2: mk::decode_step_kernel<2, true><<<grid, threads, 0, stream>>>(dp); break;
+      default: mk::decode_step_kernel<4, true><<<grid, threads, 0, stream>>>(dp); break;
+    }
+  } else {
+    switch (G) {
+      case 1: mk::decode_step_kernel<1, false><<<grid, threads, 0, stream>>>(dp); break;
+      case 2: mk::decode_step_kernel<2, false><<<grid, threads, 0, stream>>>(dp); break;
+      default: mk::decode_step_kernel<4, false><<<grid, threads, 0, stream>>>(dp); break;
+    }
   }
   return static_cast<int>(hipGetLastError());
 }

@@ -82,9 +82,13 @@ def main():
                   f"(weights at 6.4 TB/s: {sol:6.2f} us)")
         print(f"  LM    {crit[lm] - crit[lm - 1]:7.2f} us")
         lt = st[:, 1]
-        print(f"  loader FREE-wait {100 * st[:, 0].sum() / lt.sum():.1f} % of loader time; "
-              f"wave-0 FULL-wait {100 * st[:, 2].sum() / lt.sum():.1f} %; "
-              f"wave-0 poll {100 * st[:, 3].sum() / lt.sum():.1f} %")
+        if lt.sum() > 0:
+            print(f"  loader FREE-wait {100 * st[:, 0].sum() / lt.sum():.1f} % of loader time; "
+                  f"wave-0 FULL-wait {100 * st[:, 2].sum() / lt.sum():.1f} %; "
+                  f"wave-0 poll {100 * st[:, 3].sum() / lt.sum():.1f} %")
+        else:
+            print("  register-streaming mode (no loader waves): wave-0 poll "
+                  f"{st[:, 3].sum() / max(1, st.shape[0]) / 100.0:.1f} (x100 cycles per workgroup)")
         print(f"  err word {ops.decode_step_error(r.mk_sync, L)}")
     ops.set_decode_step_trace(None, None)
 
