@@ -888,6 +888,32 @@ __device__ __forceinline__ void gemv_phase_rs(PP pp, Shared& sh_, int layer, con
   }
 }
 
+// ---- attention work units --------------------------------------------------------------------
+// Only real (sequence, kv head, partition) units are enumerated, sequence-major: unit r of
+// sequence s with n_s = ceil(kvlen_s / 128) partitions is r = base_s + hk * n_s + part.  The
+// padded M x NKV x max_parts enumeration left most of the grid on empty units and packed a
+// sequence's partitions onto neighbouring workers (one workgroup's 8 waves at B >= 4).
+struct AttUnit {
+  int s, hk, part, nparts, kvlen;
+};
+template <typename PT>
+__device__ __forceinline__ int att_units(const PT& p) {
+  int total = 0;
+  for (int s = 0; s < p.M; ++s) total += p.NKV * ((p.seq_kvlen[s] + kPartTokens - 1) / kPartTokens);
+  return total;
+}
+template <typename PT>
+__device__ __forceinline__ AttUnit att_unit(const PT& p, int r) {
+  int s = 0;
+  for (;;) {  // r < att_units(p), so the walk stops at a sequence with r in range
+    const int kvlen = p.seq_kvlen[s];
+    const int n = (kvlen + kPartTokens - 1) / kPartTokens;
+    if (r < p.NKV * n) return AttUnit{s, r / n, r % n, n, kvlen};
+    r -= p.NKV * n;
+    ++s;
+  }
+}
+
 // ---- attention phase ---------------------------------------------------------------------
 template <int G>
 __device__ __forceinline__ void attention_phase(PP pp, Shared& sh_, int layer, unsigned* err) {
@@ -896,7 +922,7 @@ __device__ __forceinline__ void attention_phase(PP pp, Shared& sh_, int layer, u
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, grp = lane >> 4;
   const int P = p.max_parts;
-  const int units = p.M * p.NKV * P;
+  const int units = att_units(p);
   const int BS = 1 << p.bs_shift;
   const int64_t hs = static_cast<int64_t>(BS) * kD;
   const uint16_t* kc_l = p.k_cache + layer * p.cache_layer_elems;
@@ -908,12 +934,8 @@ __device__ __forceinline__ void attention_phase(PP pp, Shared& sh_, int layer, u
   constexpr float kNegInf = -__builtin_huge_valf();
   for (int u = blockIdx.x; u < units; u += p.G) {
     Shared& sh = fresh_lds(sh_);  // per-unit LDS addressing (no hoisted address registers)
-    const int s = u / (p.NKV * P);
-    const int hk = (u / P) % p.NKV;
-    const int part = u % P;
-    const int kvlen = p.seq_kvlen[s];
-    const int nparts = (kvlen + kPartTokens - 1) / kPartTokens;
-    if (part >= nparts) continue;  // workgroup-uniform
+    const AttUnit au = att_unit(p, u);
+    const int s = au.s, hk = au.hk, part = au.part, kvlen = au.kvlen, nparts = au.nparts;
     const int kv_begin = part * kPartTokens;
     const int kv_end = min(kvlen, kv_begin + kPartTokens);
     const int kt = kv_begin + w * 16;
@@ -1123,7 +1145,7 @@ __device__ __forceinline__ void attention_phase_w(PP pp, int layer) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, grp = lane >> 4;
   const int P = p.max_parts;
-  const int units = p.M * p.NKV * P;
+  const int units = att_units(p);
   const int BS = 1 << p.bs_shift;
   const int64_t hs = static_cast<int64_t>(BS) * kD;
   const uint16_t* kc_l = p.k_cache + layer * p.cache_layer_elems;
@@ -1134,13 +1156,11 @@ __device__ __forceinline__ void attention_phase_w(PP pp, int layer) {
   const auto ratt = dev_rsrc(p.attn);
   constexpr float kNegInf = -__builtin_huge_valf();
   const int nw = p.G * kCW;
-  for (int u = blockIdx.x * kCW + w; u < units; u += nw) {
-    const int s = u / (p.NKV * P);
-    const int hk = (u / P) % p.NKV;
-    const int part = u % P;
-    const int kvlen = p.seq_kvlen[s];
-    const int nparts = (kvlen + kPartTokens - 1) / kPartTokens;
-    if (part >= nparts) continue;  // wave-uniform
+  // workgroup index fastest: unit r -> workgroup r % G, wave r / G, so units spread over
+  // every CU's memory pipeline before any CU takes a second one
+  for (int u = w * p.G + blockIdx.x; u < units; u += nw) {
+    const AttUnit au = att_unit(p, u);
+    const int s = au.s, hk = au.hk, part = au.part, kvlen = au.kvlen, nparts = au.nparts;
     const int kv_begin = part * kPartTokens;
     const int kv_end = min(kvlen, kv_begin + kPartTokens);
     const int ntile = (kv_end - kv_begin + 15) >> 4;
