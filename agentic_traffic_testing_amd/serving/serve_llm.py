@@ -311,10 +311,16 @@ async def handle_chat(request: web.Request) -> web.Response:
         if st.s.log_requests:
             st.log(f"[llm-metrics] status=success latency_ms={latency_ms} prompt_tokens="
                    f"{prompt_tokens} completion_tokens={completion_tokens}")
+        # engine-clock split of the TTFT: arrival -> first scheduled (hold + queue) -> first
+        # token collected (prefill step); queue_wait_s minus engine_ttft_s is the hand-off from
+        # the engine thread to this handler
+        eng_ttft = final.ttft if final is not None else None
+        sched = final.queue_wait if final is not None else None
         st.records.append({"t_end": time.time(), "queue_wait_s": queue_wait,
                            "prompt_tokens": prompt_tokens,
                            "completion_tokens": completion_tokens, "burst": burst,
-                           "hold_s": st.aengine.hold_s.pop(request_id, 0.0)})
+                           "hold_s": st.aengine.hold_s.pop(request_id, 0.0),
+                           "engine_ttft_s": eng_ttft, "sched_wait_s": sched})
         meta = {
             "request_id": request_id,
             "latency_ms": latency_ms,
