@@ -24,10 +24,19 @@ def main():
     ap.add_argument("--tokens", default="512,2600")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--quantization", default="")
+    ap.add_argument("--set", action="append", default=[],
+                    help="EngineConfig override key=value (ints / floats / strings)")
+    ap.add_argument("--seqs", type=int, default=1,
+                    help="split each N into this many prompts prefilled together (5 = the "
+                         "fan-out burst shape)")
     a = ap.parse_args()
     cfg = EngineConfig(model=a.model, max_model_len=8192, max_num_batched_tokens=8192,
                        enable_prefix_caching=False, quantization=a.quantization,
                        num_kv_blocks=4096)
+    for kv in a.set:
+        k, v = kv.split("=", 1)
+        cur = getattr(cfg, k)
+        setattr(cfg, k, type(cur)(v) if not isinstance(cur, bool) else v in ("1", "true"))
     eng = LLMEngine(cfg)
     rng = np.random.default_rng(0)
     sp = SamplingParams(temperature=0.2, max_tokens=1, ignore_eos=True)
@@ -44,17 +53,18 @@ def main():
     for n in map(int, a.tokens.split(",")):
         times = []
         for r in range(a.reps + 1):
-            prompt = rng.integers(1000, 100000, size=n).tolist()
+            prompts = [rng.integers(1000, 100000, size=n // a.seqs).tolist()
+                       for _ in range(a.seqs)]
             torch.cuda.synchronize()
             if r == 1:
                 marker()
             t0 = time.perf_counter()
-            eng.generate([prompt], sp)
+            eng.generate(prompts, sp)
             torch.cuda.synchronize()
             if r:
                 times.append((time.perf_counter() - t0) * 1e3)
         marker()
-        print(f"prefill {n:6d} tokens: {statistics.median(times):8.2f} ms "
+        print(f"prefill {n:6d} tokens ({a.seqs} seqs): {statistics.median(times):8.2f} ms "
               f"({n / statistics.median(times) * 1e3:9.0f} tok/s)", flush=True)
 
 
