@@ -387,6 +387,16 @@ class LlamaModel:
     # at M 2600, bf16 gate_up+SiLU 1.06-1.10x at M 2600; everything else stays on hipBLASLt)
     _PG_AUTO = {(torch.uint8, "gate_up"): 512, (torch.uint8, "down"): 2048,
                 (torch.bfloat16, "gate_up"): 2048}
+    # row ranges where the split-K schedule (co-resident K slices of the few 256 x 256 tiles,
+    # parallel reduction) beat hipBLASLt: bf16 down+residual 1.12-1.15x at M 512 / 1024, parity
+    # at 400 (profiles/r3_prefill_gemm_ab_bf16_splitk.txt)
+    _PG_SPLITK = {(torch.bfloat16, "down"): (448, 1152)}
+
+    def _pg_splitk(self, T: int, w: torch.Tensor, proj: str) -> bool:
+        if self.prefill_gemm != "auto" or self.device.type != "cuda" or self.tp_size > 1:
+            return False
+        lo, hi = self._PG_SPLITK.get((w.dtype, proj), (1, 0))
+        return lo <= T <= hi
 
     def _pg(self, T: int, *ops_, mode: int = 0, proj: str = "") -> bool:
         """Route this prefill projection to the hand-written CDNA4 GEMM (ops.prefill_gemm):
@@ -417,6 +427,10 @@ class LlamaModel:
 
     def _proj_residual(self, x, w, scale, residual, proj=""):
         """residual += x @ w.T (row-parallel projection; TP: all-reduced partial sums)."""
+        if (scale is None and self._pg_splitk(x.shape[0], w, proj)
+                and ops.prefill_gemm_ok(x, w, ops.GEMM_RESADD)):
+            # split-K needs its T * S workgroups co-resident: TP = 1 only (one process per GPU)
+            return ops.prefill_gemm(x, w, ops.GEMM_RESADD, residual=residual, schedule="splitk")
         if scale is None and self._pg(x.shape[0], x, w, mode=ops.GEMM_RESADD, proj=proj):
             if self.tp_size > 1:
                 return self.tp_group.all_reduce_residual(ops.prefill_gemm(x, w), residual)

@@ -513,12 +513,20 @@ def prefill_gemm_ok(x: torch.Tensor, w: torch.Tensor, mode: int = GEMM_PLAIN) ->
 
 def prefill_gemm(x: torch.Tensor, w: torch.Tensor, mode: int = GEMM_PLAIN,
                  residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
-                 xs: torch.Tensor | None = None, ws: torch.Tensor | None = None) -> torch.Tensor:
+                 xs: torch.Tensor | None = None, ws: torch.Tensor | None = None,
+                 schedule: str | None = None) -> torch.Tensor:
     """Hand-written CDNA4 prefill GEMM: ``x @ w.T`` (GEMM_PLAIN), ``residual += x @ w.T`` in
     place (GEMM_RESADD; returns ``residual``) or ``silu(x @ gate.T) * (x @ up.T)`` for
     ``w = [gate; up]`` (GEMM_SILU).  bf16 operands, or fp8: uint8 e4m3fn ``x`` / ``w`` with
     fp32 row scales ``xs`` [M, 1] / ``ws`` [rows of w] (applied in the epilogue).  fp32
-    accumulate, one rounding to bf16.  CPU tensors run the PyTorch reference of the op."""
+    accumulate, one rounding to bf16.  ``schedule`` overrides the configured tile schedule
+    (prefill_gemm_config) for this call only.  CPU tensors run the PyTorch reference of the op."""
+    if schedule is not None and x.is_cuda:
+        prefill_gemm_config(schedule)
+        try:
+            return prefill_gemm(x, w, mode, residual, out, xs, ws)
+        finally:
+            prefill_gemm_config(_PG_SCHEDULE)
     n = w.shape[0] // 2 if mode == GEMM_SILU else w.shape[0]
     fp8 = x.dtype == torch.uint8
     if fp8 and (xs is None or ws is None):
@@ -551,12 +559,18 @@ def prefill_gemm(x: torch.Tensor, w: torch.Tensor, mode: int = GEMM_PLAIN,
     return out
 
 
+_PG_SCHEDULE = "hybrid"  # the configured (process-wide) schedule
+
+
 def prefill_gemm_config(schedule: str = "hybrid", group_m: int = 4, ablate: int = 0) -> None:
     """Tile schedule of the prefill GEMM: "hybrid" (data-parallel rounds + Stream-K
-    remainder), "streamk" or "dp"; ``group_m`` M tiles per raster group; ``ablate``
+    remainder), "streamk", "dp" or "splitk" (co-resident K slices of a few whole tiles with a
+    parallel reduction, where T * S fits the CUs); ``group_m`` M tiles per raster group; ``ablate``
     (measurement only, bf16 plain GEMMs): 1 no MFMA, 2 no LDS-DMA, 3 no ds_read."""
-    _native().prefill_gemm_config({"hybrid": 0, "streamk": 1, "dp": 2}[schedule], group_m,
-                                  ablate)
+    global _PG_SCHEDULE
+    _native().prefill_gemm_config({"hybrid": 0, "streamk": 1, "dp": 2, "splitk": 3}[schedule],
+                                  group_m, ablate)
+    _PG_SCHEDULE = schedule
 
 
 def prefill_gemm_error() -> int:

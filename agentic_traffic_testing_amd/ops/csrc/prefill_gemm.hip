@@ -77,6 +77,7 @@ struct GemmArgs {
   int units;                     // stream-K: phases per workgroup (last one may get fewer)
   int dp_tiles;                  // tiles [0, dp_tiles) run whole, round-robin over workgroups
   int gm;                        // tile order: groups of gm M-tiles, M fastest inside a group
+  int splitk;                    // > 1: split-K schedule (below), workgroup b = tile b / S, split b % S
   float* ws;                     // stream-K partial tiles: one 256 KB fp32 slab per workgroup
   int* flags;                    // per-workgroup "slab published" flags (consumer resets)
   unsigned* err;                 // bounded-spin timeout report
@@ -190,7 +191,17 @@ __global__ void __launch_bounds__(kThreads, 1) prefill_gemm_kernel(GemmArgs p) {
   const int64_t sk_total = static_cast<int64_t>(T - p.dp_tiles) * NP;
   const int64_t u0 = static_cast<int64_t>(vb) * p.units;
   const int64_t u1 = min(u0 + p.units, sk_total);
-  if (n_dp == 0 && u0 >= u1) return;
+  // split-K schedule (small M: a few whole tiles, e.g. 2 x 16 at M 400 for down_proj): every
+  // tile's K phases are cut into S equal slices on S co-resident workgroups (grid = T * S <=
+  // CUs, one workgroup per CU).  Each publishes the accumulator groups it does NOT reduce
+  // itself (fp32 slab, sc1 stores), arrives on the tile's counter, waits for the other S - 1,
+  // then reduces ITS 1/S of the tile's row fragments over all S slices in slice order
+  // (deterministic) and runs the epilogue for them: the reduction is spread over the S
+  // workgroups instead of one finisher reading (S - 1) whole 256 KB slabs (Stream-K's fix-up).
+  const int S = p.splitk;
+  const bool skp = S > 1;
+  const int sk_t = skp ? b / S : 0, sk_s = skp ? b % S : 0;
+  if (!skp && n_dp == 0 && u0 >= u1) return;
 
   const int dst_op = (wr ? kOpBytes : 0) + (wid & 3) * 1024;
   // fragment read offsets (fragment bases are multiples of the fragment height)
@@ -210,10 +221,15 @@ __global__ void __launch_bounds__(kThreads, 1) prefill_gemm_kernel(GemmArgs p) {
   Acc<FP8> acc;
   const int s_first = u0 < u1 ? static_cast<int>(u0 / NP) : 0;
   const int s_last = u0 < u1 ? static_cast<int>((u1 - 1) / NP) : -1;
-  for (int seg = 0; seg < n_dp + (s_last - s_first + 1); ++seg) {
+  const int nseg = skp ? 1 : n_dp + (s_last - s_first + 1);
+  for (int seg = 0; seg < nseg; ++seg) {
     int t, k0, k1;
     int64_t tu = 0;  // stream-K: first unit of tile t
-    if (seg < n_dp) {
+    if (skp) {
+      t = sk_t;
+      k0 = sk_s * (NP / S);
+      k1 = k0 + NP / S;
+    } else if (seg < n_dp) {
       t = vb + seg * nwg;
       k0 = 0;
       k1 = NP;
@@ -370,7 +386,42 @@ __global__ void __launch_bounds__(kThreads, 1) prefill_gemm_kernel(GemmArgs p) {
 
     // ---- partial tile: publish to this worker's slab ------------------------------------------
     const auto slab = dev_rsrc(p.ws);
-    if (k1 < NP) {
+    // row fragments this workgroup reduces and writes (split-K: its 1/S share)
+    constexpr int kFrags = FP8 ? 4 : 8;
+    const int i0 = skp ? sk_s * (kFrags / S) : 0;
+    const int i1 = skp ? i0 + kFrags / S : kFrags;
+    auto frag_of = [](int k) { return FP8 ? (k >> 3) : (k >> 2); };  // row fragment of group k
+    if (skp) {
+      const uint32_t base = static_cast<uint32_t>(b) * kSlabBytes;
+#pragma unroll
+      for (int k = 0; k < Acc<FP8>::kRegs; ++k)
+        if ((frag_of(k) < i0 || frag_of(k) >= i1) &&
+            tm * 256 + wr * 128 + frag_of(k) * (FP8 ? 32 : 16) < p.M)  // padding rows: never read
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(u32x4, acc.get4(k)), slab, static_cast<uint32_t>(tid * 16),
+              base + static_cast<uint32_t>(k * kThreads * 16), kScDevice);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        int* ctr = p.flags + t;
+        __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // bounded by wall clock (100 MHz): 20 ms, far past any real wait - a grid that is
+        // not co-resident (another process's kernels holding CUs) reports instead of hanging
+        const unsigned long long t_end = wall_clock64() + 2000000ull;
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < S) {
+          __builtin_amdgcn_s_sleep(1);
+          if (wall_clock64() > t_end) {
+            atomicOr(p.err, 2u);
+            break;
+          }
+        }
+        // depart; the last of the 2S adds re-arms the counter for the next launch
+        if (__hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 2 * S - 1)
+          __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+    }
+    if (!skp && k1 < NP) {
       const uint32_t base = static_cast<uint32_t>(vb) * kSlabBytes;
 #pragma unroll
       for (int k = 0; k < Acc<FP8>::kRegs; ++k)
@@ -386,7 +437,7 @@ __global__ void __launch_bounds__(kThreads, 1) prefill_gemm_kernel(GemmArgs p) {
     // are added group by group in the epilogue (adding them into the accumulators here would
     // make the register allocator copy whole accumulator tuples and spill in the main loop)
     int c0 = 0, c1 = -1;
-    if (k0 > 0) {
+    if (!skp && k0 > 0) {
       c0 = static_cast<int>(tu / p.units);
       c1 = static_cast<int>((tu + k0 - 1) / p.units);
       if (tid == 0) {
@@ -406,6 +457,18 @@ __global__ void __launch_bounds__(kThreads, 1) prefill_gemm_kernel(GemmArgs p) {
     }
     // accumulator group k (4 floats) plus the contributors' partials, in worker order
     auto part = [&](int k) {
+      if (skp) {  // the S slices of this tile in slice order, this workgroup's from registers
+        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int q = 0; q < S; ++q)
+          v += q == sk_s ? acc.get4(k)
+                         : __builtin_bit_cast(
+                               f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                          slab, static_cast<uint32_t>(tid * 16),
+                                          static_cast<uint32_t>(t * S + q) * kSlabBytes +
+                                              static_cast<uint32_t>(k * kThreads * 16),
+                                          kScDevice));
+        return v;
+      }
       f32x4 v = acc.get4(k);
       for (int cb = c0; cb <= c1; ++cb)
         v += __builtin_bit_cast(
@@ -422,7 +485,7 @@ __global__ void __launch_bounds__(kThreads, 1) prefill_gemm_kernel(GemmArgs p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = tm * 256 + wr * 128 + i * 32 + (lane & 31);
-        if (m >= p.M) continue;
+        if (i < i0 || i >= i1 || m >= p.M) continue;
         const float xsc = p.xs[m];
         uint16_t* crow = p.c + static_cast<int64_t>(m) * p.ldc;
 #pragma unroll
@@ -468,7 +531,7 @@ __global__ void __launch_bounds__(kThreads, 1) prefill_gemm_kernel(GemmArgs p) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int m = tm * 256 + wr * 128 + i * 16 + (lane & 15);
-        if (m >= p.M) continue;
+        if (i < i0 || i >= i1 || m >= p.M) continue;
         uint16_t* crow = p.c + static_cast<int64_t>(m) * p.ldc;
         if constexpr (MODE == GEMM_SILU) {
 #pragma unroll
@@ -574,13 +637,14 @@ hipError_t launch(int mode, dim3 grid, hipStream_t stream, const GemmArgs& p) {
 using namespace atta;
 
 namespace {
-int g_schedule = 0;  // 0 hybrid (data-parallel rounds + Stream-K remainder), 1 Stream-K, 2 DP
+int g_schedule = 0;  // 0 hybrid (data-parallel rounds + Stream-K remainder), 1 Stream-K, 2 DP,
+                     // 3 split-K (co-resident K slices, parallel reduction) where it fits
 int g_group_m = 4;   // M tiles per raster group
 }  // namespace
 
 // A/B knobs of the tile schedule (scripts/gpu/bench_prefill_gemm.py --schedule)
 int atta_prefill_gemm_config(int schedule, int group_m, int ablate) {
-  if (schedule < 0 || schedule > 2 || group_m < 1 || ablate < 0 || ablate > 4) return -1;
+  if (schedule < 0 || schedule > 3 || group_m < 1 || ablate < 0 || ablate > 4) return -1;
   g_schedule = schedule;
   g_group_m = group_m;
   g_ablate = ablate;
@@ -626,7 +690,19 @@ int atta_prefill_gemm(void* c, const void* a, const void* w, const void* res, in
   // schedule (auto): whole rounds of `cus` tiles data-parallel (lock-step tiles share operands
   // in L2), the remainder Stream-K (every CU the same share of its phases); measured on the
   // 8B prefill shapes (profiles/r3_prefill_gemm_ab_*)
-  if (g_schedule == 1)
+  // split-K: S = the largest power of two <= 8 (fp8: 4, its 32-row fragments) with T * S
+  // workgroups co-resident (<= CUs, one per CU) and >= 8 K phases per slice
+  p.splitk = 1;
+  if (g_schedule == 3) {
+    int S = 1;
+    while (2 * S <= (fp8 ? 4 : 8) && T * 2 * S <= cus && p.np % (2 * S) == 0 &&
+           p.np / (2 * S) >= 8)
+      S *= 2;
+    p.splitk = S;
+  }
+  if (p.splitk > 1)
+    p.dp_tiles = T;  // unused by the split-K path
+  else if (g_schedule == 1)
     p.dp_tiles = 0;  // all Stream-K
   else if (g_schedule == 2)
     p.dp_tiles = T;  // all data-parallel (last round partial)
@@ -650,6 +726,7 @@ int atta_prefill_gemm(void* c, const void* a, const void* w, const void* res, in
     workers = static_cast<int>((sk_total + p.units - 1) / p.units);
   }
   if (p.dp_tiles > 0) workers = max(workers, min(cus, p.dp_tiles));
+  if (p.splitk > 1) workers = T * p.splitk;
   p.ws = s->ws;
   p.flags = s->flags;
   p.err = s->err;

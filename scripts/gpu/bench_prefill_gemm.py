@@ -48,7 +48,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--fp8", action="store_true",
                     help="e4m3fn operands with row scales: ours vs hipBLASLt torch._scaled_mm")
-    ap.add_argument("--schedule", default="hybrid", choices=["hybrid", "streamk", "dp"])
+    ap.add_argument("--schedule", default="hybrid", choices=["hybrid", "streamk", "dp", "splitk"])
     ap.add_argument("--group-m", type=int, default=4)
     args = ap.parse_args()
     ops.prefill_gemm_config(args.schedule, args.group_m)

@@ -34,6 +34,8 @@ def timed(fn, iters=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", type=int, nargs="+", default=[400, 512])
+    ap.add_argument("--rocblas", action="store_true", help="also time rocBLAS (no split-K)")
+    ap.add_argument("--no-split", action="store_true")
     a = ap.parse_args()
     dev = "cuda"
     try:
@@ -51,7 +53,12 @@ def main():
             ref = (x.float() @ ws[0].float().t())
             base = timed(lambda i: F.linear(x, ws[i % 4]))
             row = f"{name:8s} M={m:4d} N={n:5d} K={k:5d} | linear {base:7.1f} us"
-            for s in (2, 4, 8):
+            if a.rocblas:
+                torch.backends.cuda.preferred_blas_library("cublas")  # = rocBLAS on ROCm
+                rb = timed(lambda i: F.linear(x, ws[i % 4]))
+                torch.backends.cuda.preferred_blas_library("cublaslt")
+                row += f" | rocBLAS {rb:7.1f} us (x{base / rb:4.2f})"
+            for s in (() if a.no_split else (2, 4, 8)):
                 if k % (s * 64):
                     continue
                 ks = k // s

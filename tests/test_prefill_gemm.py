@@ -151,3 +151,62 @@ def test_prefill_gemm_fp8_vs_fp32(mode, mnk):
     assert got.shape == (M, N)
     _check(got, exp, K)
     assert ops.prefill_gemm_error() == 0
+
+
+@pytest.fixture
+def splitk_schedule():
+    ops.prefill_gemm_config("splitk")
+    yield
+    ops.prefill_gemm_config("hybrid")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mnk", [(400, 4096, 14336), (77, 512, 4096), (512, 1024, 2048),
+                                 (300, 256, 512)])
+def test_prefill_gemm_splitk_vs_fp32(splitk_schedule, mode, mnk):
+    """Split-K schedule (co-resident K slices, each workgroup reducing its own row fragments
+    over every slice): the fan-out burst's down_proj shape (400 x 4096 x 14336: 32 tiles x 8
+    slices), ragged M, the smallest slice (8 phases)."""
+    assert ops.native_available(), ops._load_error
+    M, N, K = mnk
+    torch.manual_seed(M + N + K + mode)
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    rows = 2 * N if mode == ops.GEMM_SILU else N
+    w = (torch.randn(rows, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
+    if mode == ops.GEMM_RESADD:
+        r = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+        exp = _ref(x, w, mode, r)
+        got = ops.prefill_gemm(x, w, mode, residual=r)
+    else:
+        exp = _ref(x, w, mode)
+        got = ops.prefill_gemm(x, w, mode)
+    torch.cuda.synchronize()
+    _check(got, exp, K)
+    assert ops.prefill_gemm_error() == 0
+    # deterministic: the slices are summed in slice order whichever workgroup finishes last
+    if mode != ops.GEMM_RESADD:
+        again = ops.prefill_gemm(x, w, mode)
+        assert torch.equal(again, got)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_prefill_gemm_fp8_splitk_vs_fp32(splitk_schedule, mode):
+    assert ops.native_available(), ops._load_error
+    M, N, K = 400, 1024, 4096
+    torch.manual_seed(5 + mode)
+    rows = 2 * N if mode == ops.GEMM_SILU else N
+    xq, xs = _q8(torch.randn(M, K, device="cuda"))
+    wq, ws = _q8(torch.randn(rows, K, device="cuda") / K ** 0.5)
+    ws = ws.reshape(-1).contiguous()
+    if mode == ops.GEMM_RESADD:
+        r = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+        exp = _ref8(xq, xs, wq, ws, mode, r)
+        got = ops.prefill_gemm(xq, wq, mode, residual=r, xs=xs, ws=ws)
+    else:
+        exp = _ref8(xq, xs, wq, ws, mode)
+        got = ops.prefill_gemm(xq, wq, mode, xs=xs, ws=ws)
+    torch.cuda.synchronize()
+    _check(got, exp, K)
+    assert ops.prefill_gemm_error() == 0
