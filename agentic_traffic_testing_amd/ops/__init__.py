@@ -700,6 +700,12 @@ def set_attention_trace(trace=None):
     _native().set_attention_trace(trace)
 
 
+def set_gemv_trace(trace=None):
+    """Per-workgroup [start, end] timeline (100 MHz wall clock, int64 CUDA tensor of 2 words
+    per workgroup) of the NEXT decode GEMV launch only; None clears it."""
+    _native().set_gemv_trace(trace)
+
+
 def attention_decode_v2(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, scale,
                         part_out, part_lse, counters, max_parts, part_tokens, out=None,
                         num_seqs: int = -1):

@@ -526,6 +526,16 @@ void attention_decode_v2(at::Tensor out, at::Tensor part_out, at::Tensor part_ls
            "attention_decode_v2");
 }
 
+void set_gemv_trace(const c10::optional<at::Tensor>& trace) {
+  if (trace.has_value() && trace->defined()) {
+    TORCH_CHECK(trace->is_cuda() && trace->scalar_type() == at::kLong,
+                "set_gemv_trace: int64 cuda tensor");
+    atta_set_gemv_trace(trace->data_ptr());
+  } else {
+    atta_set_gemv_trace(nullptr);
+  }
+}
+
 void set_attention_trace(const c10::optional<at::Tensor>& trace) {
   if (trace.has_value()) {
     TORCH_CHECK(trace->scalar_type() == at::kLong && trace->is_contiguous() && trace->is_cuda(),
@@ -786,6 +796,7 @@ TORCH_LIBRARY(atta, m) {
   m.def("ar_buffer_bytes(int max_elems, int elem_bytes) -> int", &ar_buffer_bytes);
   m.def("ar_alloc(int bytes, int device) -> int", &ar_alloc);
   m.def("set_attention_trace(Tensor? trace) -> ()", &set_attention_trace);
+  m.def("set_gemv_trace(Tensor? trace) -> ()", &set_gemv_trace);
   m.def("ar_free(int ptr) -> ()", &ar_free);
   m.def("ar_handle(int ptr) -> Tensor", &ar_handle);
   m.def("ar_open(Tensor handle) -> int", &ar_open);

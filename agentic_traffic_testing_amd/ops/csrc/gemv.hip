@@ -36,8 +36,19 @@ namespace atta {
 template <typename T, int WAVES, int UNROLL, int MT, int EPI, bool NTL = false, bool PS = false,
           bool W8 = false>
 __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
+  unsigned long long t0 = 0;
+  if (p.wg_trace != nullptr) t0 = wall_clock64();
   skinny_body<T, WAVES, UNROLL, MT, EPI, NTL, PS, W8>(p, blockIdx.x, blockIdx.y);
+  if (p.wg_trace != nullptr) {  // timeline probe: every thread's stores issued, then one stamp
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      p.wg_trace[2 * blockIdx.x] = t0;
+      p.wg_trace[2 * blockIdx.x + 1] = wall_clock64();
+    }
+  }
 }
+
 
 // Weight-stream cache policy.  Non-temporal (nt) weight loads: every decode weight byte is
 // read once per step by one CU, so keeping it out of the caches helps - but only with the
@@ -169,6 +180,14 @@ __global__ void __launch_bounds__(kFinThreads) sample_finalize_kernel(
 }  // namespace atta
 
 using namespace atta;
+// Timeline probe for the NEXT skinny launch only (nullptr: off); see SkinnyParams.wg_trace
+static unsigned long long* g_gemv_trace = nullptr;
+void atta_set_gemv_trace(void* trace) { g_gemv_trace = static_cast<unsigned long long*>(trace); }
+static unsigned long long* take_trace() {
+  unsigned long long* t = g_gemv_trace;
+  g_gemv_trace = nullptr;
+  return t;
+}
 
 static int skinny_checks(int M, int K, int waves) {
   if (M < 1 || M > 32) return -1;
@@ -234,6 +253,7 @@ int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual
   if (const int rc = setup_split(p, waves, ksplit, N / 16, wscale != nullptr)) return rc;
   const int mt = M <= 16 ? 1 : 2;
   dim3 grid(N / 16, p.ksplit);
+  p.wg_trace = take_trace();
   if (residual != nullptr) {
     // y := residual + x W^T, computed in place on the residual buffer when y == residual;
     // otherwise copy semantics are not supported (callers pass y == residual).
@@ -282,6 +302,7 @@ int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x
   p.bs_shift = shift;
   if (const int rc = setup_split(p, waves, ksplit, p.N / 16, wscale != nullptr)) return rc;
   dim3 grid(p.N / 16, p.ksplit);
+  p.wg_trace = take_trace();
   launch_epi<EPI_QKVROPE>(dtype, M <= 16 ? 1 : 2, waves, grid, stream, p);
   return static_cast<int>(hipGetLastError());
 }
@@ -307,6 +328,7 @@ int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int 
   p.eps = eps;
   if (const int rc = setup_split(p, waves, ksplit, inter / 8, wscale != nullptr)) return rc;
   dim3 grid(inter / 8, p.ksplit);
+  p.wg_trace = take_trace();
   launch_epi<EPI_SILU>(dtype, M <= 16 ? 1 : 2, waves, grid, stream, p);
   return static_cast<int>(hipGetLastError());
 }
@@ -339,6 +361,7 @@ int atta_fused_lm_head_sample(int64_t* tokens, unsigned long long* keys, const v
   p.seeds = seeds;
   p.steps = steps;
   dim3 grid(N / 16);
+  p.wg_trace = take_trace();
   launch_epi<EPI_SAMPLE>(dtype, M <= 16 ? 1 : 2, waves, grid, stream, p);
   if (finalize == 1)
     sample_finalize_kernel<false><<<M, kFinThreads, 0, stream>>>(tokens, keys, N / 16);

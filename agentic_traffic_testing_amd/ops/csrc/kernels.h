@@ -87,6 +87,7 @@ int atta_sample_finalize(int64_t* tokens, const unsigned long long* keys, int M,
 
 // per-workgroup timeline of later decode attention launches (int64 [4 x grid]; nullptr off)
 void atta_set_attention_trace(void* trace);
+void atta_set_gemv_trace(void* trace);
 
 int atta_attention_decode_v2(void* out, float* part_out, float* part_lse, int* counters,
                              const void* q, const void* k_cache, const void* v_cache,

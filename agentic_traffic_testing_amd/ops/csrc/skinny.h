@@ -91,6 +91,9 @@ struct SkinnyParams {
   int ksplit;
   float* sk_ws;
   int* sk_counters;
+  // optional per-workgroup timeline (ops.set_gemv_trace): [start, end] on the 100 MHz wall
+  // clock per workgroup of the grid (gridDim.y == 1 launches only)
+  unsigned long long* wg_trace;
 };
 
 __device__ __forceinline__ unsigned ordered_bits(float f) {
