@@ -500,3 +500,31 @@ def test_prefill_gemm_engine_matches_oracle(model):
     assert bad <= 2
     from agentic_traffic_testing_amd import ops
     assert ops.prefill_gemm_error() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", ["small", "llama-8b-slice"])
+def test_prefill_splitk_route_engine_matches_oracle(model, monkeypatch):
+    """prefill_gemm="auto" sends bf16 down_proj steps of 448-1152 rows to the split-K schedule
+    of the hand-written GEMM (models/llama.py _PG_SPLITK); a 600-token prompt prefilled in one
+    step must take that route and still match the fp32 dense oracle (near-tie rule), with the
+    split-K wait never timing out (error word)."""
+    from agentic_traffic_testing_amd import ops
+    vocab = 30000 if model == "small" else 16000
+    cfg = EngineConfig(model=model, device="cuda", max_model_len=1024, num_kv_blocks=512,
+                       max_num_batched_tokens=1024, max_num_seqs=8,
+                       graph_batch_sizes=(1, 2, 4, 8), prefill_gemm="auto")
+    eng = LLMEngine(cfg)
+    calls = []
+    real = ops.prefill_gemm
+
+    def spy(*args, **kw):
+        calls.append(kw.get("schedule"))
+        return real(*args, **kw)
+
+    monkeypatch.setattr(ops, "prefill_gemm", spy)
+    prompts = [list(np.random.default_rng(11).integers(300, vocab, size=600))]
+    outs, bad = _check(eng, prompts, n=6, tol_logit=0.25)
+    assert bad <= 1
+    assert calls.count("splitk") == eng.runner.model.cfg.num_layers, calls
+    assert ops.prefill_gemm_error() == 0
