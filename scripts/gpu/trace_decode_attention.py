@@ -100,5 +100,11 @@ def run(ctxs, dt=torch.bfloat16):
 
 if __name__ == "__main__":
     assert ops.native_available()
-    run([3000])
-    run([3000, 3100, 2900, 3050, 2950, 0, 0, 0])
+    # CTXS="300;300,300,300,300,300" picks the batches (';' between batches, ',' inside one)
+    spec = os.environ.get("CTXS")
+    if spec:
+        for b in spec.split(";"):
+            run([int(c) for c in b.split(",")])
+    else:
+        run([3000])
+        run([3000, 3100, 2900, 3050, 2950, 0, 0, 0])
