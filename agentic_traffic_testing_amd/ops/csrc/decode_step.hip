@@ -1073,23 +1073,35 @@ __device__ __forceinline__ void attention_phase(PP pp, Shared& sh_, int layer, u
       float mr = kNegInf, wsum = 0.f;
       float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if (gidx < NG) {
-        for (int q = gidx; q < nparts; q += NG) {
-          const int64_t base = (shk * P + q) * 16 + mc;
-          const uint32_t off = static_cast<uint32_t>((base * kD + md0) * 4);
-          const float lse = dev_load4(rpl, static_cast<uint32_t>(base * 4));
-          const f32x4 pa = __builtin_bit_cast(f32x4, dev_load16(rpo, off));
-          const f32x4 pb = __builtin_bit_cast(f32x4, dev_load16(rpo, off + 16));
-          if (lse == kNegInf) continue;
-          const float m_new = fmaxf(mr, lse);
-          const float sc = exp2f(mr - m_new);
-          const float wt = exp2f(lse - m_new);
-          wsum = wsum * sc + wt;
+        // partitions gidx, gidx + NG, ... folded in order; their loads go out 4 at a time
+        // (one dependent sc1 round trip per 4 partitions, not per partition)
+        constexpr int PB = 4;
+        for (int q0 = gidx; q0 < nparts; q0 += PB * NG) {
+          float lse[PB];
+          f32x4 pa[PB], pb[PB];
 #pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            acc[jj] = acc[jj] * sc + wt * pa[jj];
-            acc[4 + jj] = acc[4 + jj] * sc + wt * pb[jj];
+          for (int u = 0; u < PB; ++u) {
+            const int q = min(q0 + u * NG, nparts - 1);
+            const int64_t base = (shk * P + q) * 16 + mc;
+            const uint32_t off = static_cast<uint32_t>((base * kD + md0) * 4);
+            lse[u] = dev_load4(rpl, static_cast<uint32_t>(base * 4));
+            pa[u] = __builtin_bit_cast(f32x4, dev_load16(rpo, off));
+            pb[u] = __builtin_bit_cast(f32x4, dev_load16(rpo, off + 16));
           }
-          mr = m_new;
+#pragma unroll
+          for (int u = 0; u < PB; ++u) {
+            if (q0 + u * NG >= nparts || lse[u] == kNegInf) continue;
+            const float m_new = fmaxf(mr, lse[u]);
+            const float sc = exp2f(mr - m_new);
+            const float wt = exp2f(lse[u] - m_new);
+            wsum = wsum * sc + wt;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              acc[jj] = acc[jj] * sc + wt * pa[u][jj];
+              acc[4 + jj] = acc[4 + jj] * sc + wt * pb[u][jj];
+            }
+            mr = m_new;
+          }
         }
       }
       cbar(sh, err);  // as.* (aliased by ms) fully consumed by every merger thread above
@@ -1273,23 +1285,35 @@ __device__ __forceinline__ void attention_phase_w(PP pp, int layer) {
     if (mc < G) {
       float mr = kNegInf, wsum = 0.f;
       float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int q = 0; q < nparts; ++q) {
-        const int64_t pbase = (shk * P + q) * 16 + mc;
-        const float lse = dev_load4(rpl, static_cast<uint32_t>(pbase * 4));
-        const uint32_t off = static_cast<uint32_t>((pbase * kD + md0) * 4);
-        const f32x4 pa = __builtin_bit_cast(f32x4, dev_load16(rpo, off));
-        const f32x4 pb = __builtin_bit_cast(f32x4, dev_load16(rpo, off + 16));
-        if (lse == kNegInf) continue;
-        const float m_new = fmaxf(mr, lse);
-        const float sc = exp2f(mr - m_new);
-        const float wt = exp2f(lse - m_new);
-        wsum = wsum * sc + wt;
+      // every partition in order; loads 8 partitions at a time (one dependent sc1 round trip
+      // per 8 instead of per partition: 8 partitions at B = 5, ctx 1000)
+      constexpr int PB = 8;
+      for (int q0 = 0; q0 < nparts; q0 += PB) {
+        float lse[PB];
+        f32x4 pa[PB], pb[PB];
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          acc[jj] = acc[jj] * sc + wt * pa[jj];
-          acc[4 + jj] = acc[4 + jj] * sc + wt * pb[jj];
+        for (int u = 0; u < PB; ++u) {
+          const int q = min(q0 + u, nparts - 1);
+          const int64_t pbase = (shk * P + q) * 16 + mc;
+          const uint32_t off = static_cast<uint32_t>((pbase * kD + md0) * 4);
+          lse[u] = dev_load4(rpl, static_cast<uint32_t>(pbase * 4));
+          pa[u] = __builtin_bit_cast(f32x4, dev_load16(rpo, off));
+          pb[u] = __builtin_bit_cast(f32x4, dev_load16(rpo, off + 16));
         }
-        mr = m_new;
+#pragma unroll
+        for (int u = 0; u < PB; ++u) {
+          if (q0 + u >= nparts || lse[u] == kNegInf) continue;
+          const float m_new = fmaxf(mr, lse[u]);
+          const float sc = exp2f(mr - m_new);
+          const float wt = exp2f(lse[u] - m_new);
+          wsum = wsum * sc + wt;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            acc[jj] = acc[jj] * sc + wt * pa[u][jj];
+            acc[4 + jj] = acc[4 + jj] * sc + wt * pb[u][jj];
+          }
+          mr = m_new;
+        }
       }
       const float inv = wsum > 0.f ? 1.f / wsum : 0.f;
       u32x4 o8;
