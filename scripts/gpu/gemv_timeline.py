@@ -120,12 +120,17 @@ def main():
         med_end = float(en.median())
         gap = float(st.min()) - prev_end if prev_end is not None else float("nan")
         window = float(en.max() - st.min())
+        if window <= 0:  # launch without the probe (e.g. the persistent gate_up variant)
+            print(f"{name:10s} {grid:5d}   (no timeline)")
+            prev_end = None
+            rows.append((float("nan"), 0.0, 0.0, 0.0, 0.0))
+            continue
         rows.append((gap, float(st.max() - st.min()), float((en - st).median()),
                      float(en.max()) - med_end, window))
         print(f"{name:10s} {grid:5d} {gap:6.2f} {rows[-1][1]:7.2f} {rows[-1][2]:7.2f} "
               f"{rows[-1][3]:6.2f} {window:7.2f} {nbytes / window / 1e6:5.2f}")
         prev_end = float(en.max())
-    gaps = [r[0] for r in rows[1:]]
+    gaps = [r[0] for r in rows[1:] if r[0] == r[0]] or [0.0]
     print(f"# chain span {prev_end - first:.1f} us; launch gaps sum {sum(gaps):.1f} us "
           f"(median {statistics.median(gaps):.2f}); dispatch spreads sum "
           f"{sum(r[1] for r in rows):.1f}; drains sum {sum(r[3] for r in rows):.1f}")

@@ -737,3 +737,18 @@ def test_fp8_decode_kernels_vs_fp32_reference(m):
     close(got, exp, 3e-2, 3e-2)
     close(kc, kc_r, 3e-2, 3e-2)
     close(vc, vc_r, 3e-2, 3e-2)
+
+
+@pytest.mark.parametrize("m", [1, 5, 16])
+def test_decode_gate_up_silu_8b_shape(m):
+    """gate_up + SiLU at the Llama-3.1-8B decode shape (inter 14336, K 4096, pre-shuffled):
+    1792 tiles - a multiple of the CU count, so with ATTA_GU_PERSIST=1 this runs the
+    persistent one-pipeline-per-CU variant (gemv.hip silu_persist_kernel) - vs fp32."""
+    torch.manual_seed(m)
+    dt = torch.bfloat16
+    inter, H = 14336, 4096
+    x = torch.randn(m, H, dtype=dt, device="cuda")
+    wg = torch.randn(2 * inter, H, dtype=dt, device="cuda") * 0.02
+    exp = ref.silu_and_mul(torch.nn.functional.linear(_norm_ref(x).float(), wg.float()))
+    got = ops.decode_gate_up_silu(x, ops.preshuffle(wg, "silu"), 1e-5, preshuffled=True)
+    close(got, exp.to(dt), 4e-2, 4e-2)
