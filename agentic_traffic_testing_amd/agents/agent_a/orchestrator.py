@@ -200,6 +200,7 @@ ORACLE_ROLES = [
     ("critic", "Find errors, gaps and risks in the work"),
     ("summarizer", "Condense the results into a clear answer"),
 ]
+assert tuple(r for r, _ in ORACLE_ROLES) == P.ROLES  # the recruitment prompt's vocabulary
 
 
 def oracle_recruitment(task_id: str, iteration: int, max_experts: int) -> dict:
@@ -219,16 +220,20 @@ def oracle_recruitment(task_id: str, iteration: int, max_experts: int) -> dict:
     }
 
 
-def oracle_evaluation(task_id: str, iteration: int) -> dict:
+def oracle_evaluation(task_id: str, iteration: int, threshold: int = 80) -> dict:
+    """Seeded evaluator reply in the EVALUATION_PROMPT schema: criteria 0-100, overall score
+    = their weighted average with the prompt's weights (30/30/15/15/10)."""
     rng = random.Random(hashlib.sha256(f"{task_id}:{iteration}:e".encode()).hexdigest())
-    crit = {k: rng.randint(10, 20) for k in
-            ("completeness", "correctness", "clarity", "relevance", "actionability")}
-    score = sum(crit.values())
-    return {"goal_achieved": score >= 80, "score": score, "criteria": crit,
-            "rationale": "oracle: sum of seeded criterion scores",
-            "feedback": "" if score >= 80 else "Tighten correctness and cover missing steps.",
-            "missing_aspects": [] if score >= 80 else ["verification of results"],
-            "should_iterate": score < 80}
+    crit = {k: rng.randint(50, 100) for k in P.CRITERIA_WEIGHTS}
+    score = int(round(sum(P.CRITERIA_WEIGHTS[k] * v for k, v in crit.items())))
+    ok = score >= threshold
+    return {"goal_achieved": ok, "score": score, "criteria": crit,
+            "rationale": "oracle: weighted average of seeded criterion scores "
+                         "(completeness 30%, correctness 30%, clarity 15%, relevance 15%, "
+                         "actionability 10%)",
+            "feedback": "" if ok else "Tighten correctness and cover missing steps.",
+            "missing_aspects": [] if ok else ["verification of results"],
+            "should_iterate": not ok}
 
 
 class AgentVerseOrchestrator:
@@ -630,7 +635,8 @@ class AgentVerseOrchestrator:
         max_model_len - eval_max_tokens - margin; falls back to a character budget."""
         def render(res):
             return P.EVALUATION.format(task=st.original_task, iteration=st.iteration + 1,
-                                       max_iterations=st.max_iterations, results=res)
+                                       max_iterations=st.max_iterations, results=res,
+                                       success_threshold=st.success_threshold)
         budget = self.max_model_len - self.eval_max_tokens - self.margin
         prompt = render(results)
         truncated, trimmed, final_tokens = False, None, None
@@ -676,7 +682,7 @@ class AgentVerseOrchestrator:
             if not isinstance(parsed, dict):
                 parsed = parse_markdown_fields(resp) or {}
             if self.oracle and "score" not in parsed:
-                parsed = oracle_evaluation(st.task_id, st.iteration)
+                parsed = oracle_evaluation(st.task_id, st.iteration, st.success_threshold or 80)
                 st.llm_requests[-1]["oracle"] = True
             try:
                 score = max(0, min(100, int(parsed.get("score"))))

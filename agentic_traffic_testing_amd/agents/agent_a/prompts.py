@@ -1,140 +1,212 @@
-"""Prompt templates for the AgentVerse workflow (role of reference agents/agent_a/prompts.py).
+"""Prompt templates for the AgentVerse workflow.
 
-Eight templates drive the 4-stage loop (recruitment, horizontal discussion, vertical
-solver / reviewer, execution, evaluation, discussion synthesis, final synthesis).  The
-wording is this repo's own; what the workflow depends on is preserved: the JSON schemas
-the parsers expect (``experts`` / ``communication_structure`` / ``execution_order`` /
-``reasoning`` for recruitment; ``goal_achieved`` / ``score`` / ``criteria`` / ``rationale``
-/ ``feedback`` / ``missing_aspects`` / ``should_iterate`` for evaluation) and the
-``[CONSENSUS]`` / ``[APPROVED]`` markers the discussion loops look for.
+The text of these templates is workload contract data, not code style: it sets the prompt
+sizes (L7 bytes, prompt tokens, prefill time) of every config-4 LLM call the testbed
+measures, and the role vocabulary the solver selection depends on (``e.role == "planner"``,
+reference agents/agent_a/orchestrator.py:1195).  It is therefore reproduced as the reference
+defines it (reference agents/agent_a/prompts.py:8-192), including the fixed 5-role
+vocabulary, the ``{success_threshold}`` slot and the weighted-criteria evaluation prompt.
+``tests/test_agent_prompts.py`` pins every template's placeholders and length.
 """
 
-RECRUITMENT = """You coordinate a team of specialist agents. Study the task and decide which \
-experts (between 2 and 5) should work on it and how they should communicate.
+EXPERT_RECRUITMENT_PROMPT = """You are the Orchestrator (Agent A) in an AgentVerse multi-agent system.
+Your job is to analyze the user's task and determine what expert agents are needed.
 
-Task:
+User Task:
 {task}
+
 {feedback_context}
-Communication structures:
-- "horizontal": every expert contributes to an open discussion until they agree.
-- "vertical": one solver drafts a plan, the other experts review it, the solver revises.
 
-Reply with JSON only:
-{{
-  "experts": [
-    {{"role": "<short role name>", "responsibilities": "<what this expert covers>",
-      "contract": "<instructions that bind this expert>"}}
-  ],
-  "communication_structure": "horizontal" or "vertical",
-  "execution_order": ["<role>", "..."],
-  "reasoning": "<one or two sentences on why this team and structure>"
-}}"""
+Based on this task, determine:
+1. What specialized roles are needed? Choose from: planner, researcher, executor, critic, summarizer
+2. How many instances of each role (1-3 per role, max 5 total agents)?
+3. What specific responsibilities should each role have?
+4. Should agents use horizontal (democratic discussion) or vertical (solver + reviewers) communication?
 
-HORIZONTAL_DISCUSSION = """Role: {role}
-Contract: {contract}
+IMPORTANT: Return ONLY valid JSON with no extra text.
+The JSON MUST have this shape (types, not examples):
+- "experts": list of objects, each with:
+  - "role": one of ["planner", "researcher", "executor", "critic", "summarizer"]
+  - "responsibilities": string describing what this expert will do
+  - "contract": string with detailed instructions for this expert
+- "communication_structure": "horizontal" or "vertical"
+- "execution_order": list of role names in the order they should act
+- "reasoning": brief string explaining why these experts and structure were chosen
+"""
 
-Team task:
+HORIZONTAL_DISCUSSION_PROMPT = """You are a {role} agent in a collaborative multi-agent discussion.
+
+Your Contract:
+{contract}
+
+Original Task:
 {task}
 
-Discussion so far (round {round_num}):
+Discussion History:
 {discussion_history}
 
-Add your view: propose concrete steps, point out problems with earlier suggestions and \
-refine them. If you agree with the current plan and have nothing to add, end your message \
-with [CONSENSUS]."""
+Current Round: {round_num}
 
-VERTICAL_SOLVER = """You are the solver for this team.
-Contract: {contract}
+Provide your expert input on this task. Consider what others have said.
+If you believe consensus has been reached and no more input is needed, end your response with [CONSENSUS].
+Otherwise, provide constructive input that moves toward a solution.
+"""
 
-Task:
-{task}
-{previous_proposal}{critiques}
-Write a complete, step-by-step proposal that solves the task. If reviewer critiques are \
-shown above, address every one of them explicitly."""
+VERTICAL_SOLVER_PROMPT = """You are the Solver agent. Your job is to propose a solution.
 
-VERTICAL_REVIEWER = """Role: {role} (reviewer)
-Contract: {contract}
+Your Contract:
+{contract}
 
-Task:
+Original Task:
 {task}
 
-Proposal under review:
+{previous_proposal}
+{critiques}
+
+Propose a detailed solution to the task. Be specific and actionable.
+"""
+
+VERTICAL_REVIEWER_PROMPT = """You are a {role} Reviewer agent. Your job is to critique the proposed solution.
+
+Your Contract:
+{contract}
+
+Original Task:
+{task}
+
+Proposed Solution:
 {proposal}
 
-Check the proposal for errors, gaps and risks from your role's point of view and list \
-specific fixes. If the proposal is acceptable as written, end your reply with [APPROVED]."""
+Review this proposal critically:
+- Is it correct and complete?
+- Are there any errors or missing aspects?
+- What improvements would you suggest?
 
-EXECUTION = """Role: {role}
-Contract: {contract}
+If the proposal is acceptable, respond with [APPROVED].
+Otherwise, provide specific, constructive criticism.
+"""
 
-Overall task:
+EXECUTION_PROMPT = """You are an {role} agent executing a specific subtask.
+
+Your Contract:
+{contract}
+
+Original Task:
 {task}
 
-Agreed approach (excerpt):
-{decision_context}
-
-Your assignment:
+Your Assigned Subtask:
 {subtask}
 
-Carry out your assignment now and report the concrete result."""
+Context from Decision Phase:
+{decision_context}
 
-EVALUATION = """You are the evaluator of a multi-agent run. Judge whether the team's \
-combined output accomplishes the task.
+Execute your subtask and provide a detailed result. Be specific and thorough.
+"""
 
-Task:
+EVALUATION_PROMPT = """You are the Evaluator agent. Assess whether the goal has been achieved.
+
+Original Task:
 {task}
+
+Agent Results:
+{results}
 
 Iteration: {iteration} of {max_iterations}
+Success threshold (score to accept and stop): {success_threshold}/100
 
-Outputs from the experts:
-{results}
+Evaluate the results using the following criteria:
+1. **Completeness** (0-100): Does the solution fully address all aspects of the task?
+2. **Correctness** (0-100): Is the information accurate and factually correct?
+3. **Clarity** (0-100): Is the solution well-structured, clear, and easy to understand?
+4. **Relevance** (0-100): Does the solution stay focused on the task requirements?
+5. **Actionability** (0-100): If applicable, is the solution practical and implementable?
 
-Score each criterion from 0 to 20 (completeness, correctness, clarity, relevance, \
-actionability); the overall score is their sum (0-100).  Reply with JSON only:
-{{
-  "goal_achieved": true or false,
-  "score": <0-100>,
-  "criteria": {{"completeness": <0-20>, "correctness": <0-20>, "clarity": <0-20>,
-               "relevance": <0-20>, "actionability": <0-20>}},
-  "rationale": "<how the score was reached>",
-  "feedback": "<what the next iteration should change>",
-  "missing_aspects": ["<gap>", "..."],
-  "should_iterate": true or false
-}}"""
+Calculate an overall score (0-100) as a weighted average using the below weights:
+- Completeness: 30%
+- Correctness: 30%
+- Clarity: 15%
+- Relevance: 15%
+- Actionability: 10%
 
-SYNTHESIZE_DISCUSSION = """Summarise the team discussion below into one decision the \
-experts can execute.
+Also assess:
+- Is the original task fully addressed? (yes/no)
+- What aspects are missing or could be improved?
+- Should we iterate with adjusted experts?
 
-Task:
+IMPORTANT: Return ONLY valid JSON with this exact structure:
+
+Required fields:
+- "goal_achieved": boolean - whether the original task is fully addressed
+- "score": integer 0-100 - overall quality score calculated as weighted average:
+  * Completeness: 30% weight
+  * Correctness: 30% weight
+  * Clarity: 15% weight
+  * Relevance: 15% weight
+  * Actionability: 10% weight
+- "criteria": object with integer values 0-100 for each:
+  * "completeness": integer 0-100
+  * "correctness": integer 0-100
+  * "clarity": integer 0-100
+  * "relevance": integer 0-100
+  * "actionability": integer 0-100
+- "rationale": string - explanation of how the overall score was calculated based on the criteria
+- "feedback": string - REQUIRED when score is below threshold: actionable guidance for the next iteration's recruitment (e.g. which expert types to add/change, what gaps to address). Always provide this when score < {success_threshold} so the next iteration can improve.
+- "missing_aspects": array of strings - aspects that are missing or could be improved (empty array [] if none)
+- "should_iterate": boolean - whether to iterate with adjusted experts
+
+Evaluate honestly based on the actual quality of the results. Do not bias toward any particular score range.
+"""
+
+FINAL_SYNTHESIS_PROMPT = """You are the Orchestrator producing the FINAL COMPLETE ANSWER for the user.
+
+Original Task:
 {task}
 
-Discussion transcript:
-{discussion_history}
-
-State the agreed approach as a numbered plan and note any point that is still disputed."""
-
-FINAL_SYNTHESIS = """Produce the final answer for the user from the team's work.
-
-Task:
-{task}
-
-Iterations:
+Iteration History:
 {iteration_summary}
 
-Expert results:
+Final Agent Results:
 {results}
 
-Last evaluation:
+Evaluation:
 {evaluation}
 
-Write one coherent, self-contained response that answers the task directly."""
+IMPORTANT INSTRUCTIONS:
+1. Produce a COMPLETE, STANDALONE answer that fully addresses the original task
+2. The user will ONLY see this final output - they will NOT see the agent results above
+3. Include ALL functional details, code, steps, explanations, or solutions from the agent results
+4. Do NOT summarize or truncate - include the FULL content needed to answer the task
+5. Structure the answer clearly with sections/headings if appropriate
+6. If the task asked for code, include the COMPLETE code (not snippets or partial examples)
+7. If the task asked for steps/instructions, include ALL steps with full details
+8. The answer must make complete sense on its own without any additional context
 
-# reference-style aliases (agents/agent_a/prompts.py names)
-EXPERT_RECRUITMENT_PROMPT = RECRUITMENT
-HORIZONTAL_DISCUSSION_PROMPT = HORIZONTAL_DISCUSSION
-VERTICAL_SOLVER_PROMPT = VERTICAL_SOLVER
-VERTICAL_REVIEWER_PROMPT = VERTICAL_REVIEWER
-EXECUTION_PROMPT = EXECUTION
-EVALUATION_PROMPT = EVALUATION
-FINAL_SYNTHESIS_PROMPT = FINAL_SYNTHESIS
-SYNTHESIZE_DISCUSSION_PROMPT = SYNTHESIZE_DISCUSSION
+Produce the complete final answer now:
+"""
+
+SYNTHESIZE_DISCUSSION_PROMPT = """You are the Orchestrator. Synthesize the discussion into a clear action plan.
+
+Original Task:
+{task}
+
+Discussion:
+{discussion_history}
+
+Provide a clear, actionable summary of what should be done based on the discussion.
+"""
+
+# the 5-role vocabulary the recruitment prompt offers (and the oracle draws from)
+ROLES = ("planner", "researcher", "executor", "critic", "summarizer")
+# evaluation criterion weights stated in EVALUATION_PROMPT
+CRITERIA_WEIGHTS = {"completeness": 0.30, "correctness": 0.30, "clarity": 0.15,
+                    "relevance": 0.15, "actionability": 0.10}
+
+# short names used by the orchestrator
+RECRUITMENT = EXPERT_RECRUITMENT_PROMPT
+HORIZONTAL_DISCUSSION = HORIZONTAL_DISCUSSION_PROMPT
+VERTICAL_SOLVER = VERTICAL_SOLVER_PROMPT
+VERTICAL_REVIEWER = VERTICAL_REVIEWER_PROMPT
+EXECUTION = EXECUTION_PROMPT
+EVALUATION = EVALUATION_PROMPT
+FINAL_SYNTHESIS = FINAL_SYNTHESIS_PROMPT
+SYNTHESIZE_DISCUSSION = SYNTHESIZE_DISCUSSION_PROMPT

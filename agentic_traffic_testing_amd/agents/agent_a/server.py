@@ -27,6 +27,7 @@ from __future__ import annotations
 import json
 import os
 import threading
+import time
 from concurrent.futures import ThreadPoolExecutor, as_completed
 from datetime import datetime, timezone
 from urllib.parse import parse_qs, urlparse
@@ -379,7 +380,15 @@ class AgentAHandler(JsonHandler):
                         sp.set_attribute("app.agent_role", role)
                     headers = tracing.inject({"x-agent-index": str(idx)})
                     headers["X-Task-ID"] = run.task_id
-                    headers["x-fanout"] = str(len(workers))  # burst-aware LLM admission
+                    # x-fanout: additive header for the backend's burst-aware admission
+                    # (docs/agents.md); AGENT_FANOUT_HEADER=0 keeps the L7 bytes reference-exact
+                    if os.environ.get("AGENT_FANOUT_HEADER", "1") != "0":
+                        headers["x-fanout"] = str(len(workers))
+                    # AGENT_FANOUT_STAGGER_MS: worker i's call leaves i * ms late - an L7
+                    # arrival-skew knob for burst experiments (netem skews at L3)
+                    stagger = env_float("AGENT_FANOUT_STAGGER_MS", 0.0) / 1000.0
+                    if stagger > 0:
+                        time.sleep(stagger * (idx - 1))
                     return client.call_agent_b(sub, scenario=run.scenario, headers=headers,
                                                agent_b_role=role,
                                                agent_b_contract=w["contract"] or r["b_contract"],

@@ -109,7 +109,7 @@ def _proxy_session(url: str, idx: int, turns: int, max_tokens: int) -> int:
 
 def run_e2e(engine, steps: int, warmup: int, fanout: int = 5, max_tokens: int = 512,
             log=None, workload: str = "agentic_parallel", max_tokens_limit: int = 0,
-            proxy_turns: int = 4) -> dict:
+            proxy_turns: int = 4, arrival_skew_ms: float = 0.0) -> dict:
     from ..agents.common.http import shared_ssl_context
     from ..testing.stack import Stack
 
@@ -119,7 +119,9 @@ def run_e2e(engine, steps: int, warmup: int, fanout: int = 5, max_tokens: int = 
            "LLM_MAX_MODEL_LEN": str(engine.cfg.max_model_len),
            "AGENT_B_TIMEOUT_SECONDS": "1200", "LLM_TIMEOUT_SECONDS": "1200",
            "AGENTVERSE_LLM_TIMEOUT_SECONDS": "1200", "LOG_LLM_REQUESTS": "0",
-           "LLM_MAX_TOKENS_LIMIT": str(max_tokens_limit), "AGENTVERSE_ORACLE": "1"}
+           "LLM_MAX_TOKENS_LIMIT": str(max_tokens_limit), "AGENTVERSE_ORACLE": "1",
+           # Agent A staggers fan-out worker i by i * ms (L7 arrival skew, burst experiments)
+           "AGENT_FANOUT_STAGGER_MS": str(arrival_skew_ms)}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)  # Settings() of the backend reads them at construction
     proxy = None

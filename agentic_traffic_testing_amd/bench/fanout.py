@@ -67,6 +67,8 @@ class EpisodeResult:
     latencies: list = field(default_factory=list)
     seconds: float = 0.0
     requests: int = 0
+    # per phase (planning / burst / final): (name, prompt tokens, cached tokens, TTFTs)
+    phases: list = field(default_factory=list)
 
 
 class FanoutWorkload:
@@ -90,7 +92,7 @@ class FanoutWorkload:
         return SamplingParams(temperature=self.temperature, max_tokens=self.max_tokens,
                               ignore_eos=True, seed=int(self.rng.integers(1 << 62)))
 
-    def _run_phase(self, prompts: list[list[int]], res: EpisodeResult) -> list:
+    def _run_phase(self, prompts: list[list[int]], res: EpisodeResult, name: str = "") -> list:
         eng = self.engine
         t_arr = time.perf_counter()
         rids = []
@@ -111,19 +113,21 @@ class FanoutWorkload:
             res.ttfts.append(o.ttft)
             res.latencies.append(o.finish_time - o.arrival_time)
             res.requests += 1
+        res.phases.append((name, sum(o.prompt_tokens for o in outs),
+                           sum(o.cached_prompt_tokens for o in outs), [o.ttft for o in outs]))
         return outs
 
     def run_episode(self) -> EpisodeResult:
         task = TASKS[self.episode_idx % len(TASKS)] + f" (episode {self.episode_idx})"
         res = EpisodeResult()
         t0 = time.perf_counter()
-        self._run_phase([self._encode(planning_prompt(task, self.fanout))], res)
+        self._run_phase([self._encode(planning_prompt(task, self.fanout))], res, "planning")
         subtasks = [f"Subtask {i}: {task}" for i in range(1, self.fanout + 1)]
         worker_ids = [self._encode(worker_prompt(s, AGENT_B_ROLES[i % len(AGENT_B_ROLES)]))
                       for i, s in enumerate(subtasks)]
-        outs = self._run_phase(worker_ids, res)
+        outs = self._run_phase(worker_ids, res, "burst")
         reports = [self.tok.decode(o.token_ids) for o in outs]
-        self._run_phase([self._encode(final_prompt(task, reports))], res)
+        self._run_phase([self._encode(final_prompt(task, reports))], res, "final")
         res.seconds = time.perf_counter() - t0
         self.episode_idx += 1
         return res

@@ -212,6 +212,9 @@ class EngineConfig:
     # (X-Task-ID + x-fanout headers) are held up to this long for their siblings so the
     # burst shares one prefill; 0 disables.  Requests without the headers are never held.
     burst_window_ms: float = 10.0
+    # ... and the window closes early once this long has passed since the burst's latest
+    # arrival (a LAN fan-out lands inside ~1 ms; under netem skew early arrivals go ahead)
+    burst_gap_ms: float = 4.0
     # prefill projection GEMMs: "hipblaslt", "atta" (hand-written CDNA4 Stream-K GEMM with
     # fused residual-add / SiLU-mul epilogues, bf16 and fp8: ops/csrc/prefill_gemm.hip, for
     # steps of >= prefill_gemm_min_rows tokens) or "auto" (each projection on whichever won

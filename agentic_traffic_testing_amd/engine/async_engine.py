@@ -13,7 +13,12 @@ request that carries its burst (``burst=(key, size)``: the X-Task-ID and the fan
 Agent B forwards as ``x-fanout``) is held until its siblings are in or ``burst_window_s``
 has passed since the burst's first arrival, then the whole group is admitted together and
 shares ONE prefill forward.  Requests without burst information are never delayed.  TTFT
-still runs from each request's arrival, hold time included.
+still runs from each request's arrival, hold time included.  The window also closes early
+once ``burst_gap_s`` has passed since the burst's LATEST arrival: a LAN fan-out lands its
+siblings well inside that gap, while under arrival skew (netem delay / jitter on the agents,
+scripts/traffic/apply_network_emulation.sh) a lone early request is not held for siblings
+that are still tens of ms away - it goes ahead alone and the stragglers join the running
+batch on arrival.
 
 Watchdog (SURVEY §5.3): ``heartbeat`` is refreshed every loop iteration;
 ``stalled(threshold)`` is true when work is pending but the loop has not progressed for
@@ -36,13 +41,20 @@ class EngineDeadError(RuntimeError):
 
 
 class AsyncEngine:
+    # a flushed burst's record of expected stragglers lives this long
+    FLUSHED_TTL_S = 2.0
+
     def __init__(self, engine: LLMEngine, on_step=None, stream_interval_s: float = 0.05,
-                 burst_window_s: float | None = None):
+                 burst_window_s: float | None = None, burst_gap_s: float | None = None):
         self.engine = engine
         if burst_window_s is None:
             burst_window_s = getattr(engine.cfg, "burst_window_ms", 0.0) / 1000.0
+        if burst_gap_s is None:
+            burst_gap_s = getattr(engine.cfg, "burst_gap_ms", 4.0) / 1000.0
         self.burst_window_s = max(0.0, float(burst_window_s))
-        # held bursts: key -> [deadline, expected size, [pending entries in arrival order]]
+        self.burst_gap_s = max(0.0, float(burst_gap_s))
+        # held bursts: key -> [deadline, expected size, [pending entries in arrival order],
+        # window deadline (first arrival + window)]
         self._held: dict[str, list] = {}
         # bursts flushed at their deadline: key -> [stragglers still expected, expiry]; a
         # late sibling is admitted at once instead of opening a new window
@@ -147,8 +159,8 @@ class AsyncEngine:
     def _fail_pending(self, err: BaseException):
         while self._pending:
             self._deliver(self._pending.popleft()[0], err)
-        for _, _, group in self._held.values():
-            for entry in group:
+        for held in self._held.values():
+            for entry in held[2]:
                 self._deliver(entry[0], err)
         self._held.clear()
 
@@ -159,9 +171,17 @@ class AsyncEngine:
         except Exception as e:  # bad request: fail only that one
             self._deliver(rid, e)
 
+    def _deadline(self, window_end: float, last_arrival: float) -> float:
+        if self.burst_gap_s > 0:
+            return min(window_end, last_arrival + self.burst_gap_s)
+        return window_end
+
     def _take_pending(self, now: float) -> float | None:
-        """Move arrived requests into the engine - bursts held until complete or expired.
-        Returns the earliest pending burst deadline (None: nothing held)."""
+        """Move arrived requests into the engine - bursts held until complete, until the
+        window closes, or until no sibling arrived for ``burst_gap_s``.  Returns the earliest
+        pending burst deadline (None: nothing held)."""
+        for key in [k for k, v in self._flushed.items() if now > v[1]]:
+            del self._flushed[key]  # stragglers that never came (failed agent, disconnect)
         while self._pending:
             entry = self._pending.popleft()
             burst = entry[4] if len(entry) > 4 else None
@@ -178,15 +198,16 @@ class AsyncEngine:
                 continue
             g = self._held.get(key)
             if g is None:
-                g = self._held[key] = [entry[3] + self.burst_window_s, size, []]
+                g = self._held[key] = [0.0, size, [], entry[3] + self.burst_window_s]
             g[2].append(entry)
+            g[0] = self._deadline(g[3], entry[3])
         nearest = None
         for key in list(self._held):
-            deadline, size, group = self._held[key]
+            deadline, size, group = self._held[key][:3]
             if len(group) >= size or now >= deadline:
                 del self._held[key]
                 if len(group) < size:
-                    self._flushed[key] = [size - len(group), now + 30.0]
+                    self._flushed[key] = [size - len(group), now + self.FLUSHED_TTL_S]
                 if len(self.hold_s) > 4096:  # callers that never pop: stay bounded
                     self.hold_s.clear()
                 for entry in group:  # arrival order: FIFO admission within the burst

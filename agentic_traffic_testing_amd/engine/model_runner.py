@@ -174,6 +174,9 @@ class ModelRunner:
         self.tok_host = [torch.zeros(max(cfg.max_num_seqs, 256), dtype=torch.int64,
                                      pin_memory=pin) for _ in range(2)]
         self._tok_done = [torch.cuda.Event() if self.is_cuda else None for _ in range(2)]
+        # the prefill GEMM's error word as of the last prefill step (0: every wait succeeded)
+        self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=pin)
+        self.kernel_error = 0
         self._last_collect = 0.0
         nkv = self.model.n_kv_heads
         self.part_out = torch.empty(self.max_seqs * nkv * alloc_parts * 16 * 128,
@@ -458,7 +461,18 @@ class ModelRunner:
         if self.publisher is not None:
             self.publisher.publish(np.concatenate([hdr, host]))
         toks = self._run(hdr)
-        return toks[:n].cpu().numpy()
+        if self.is_cuda and lay.T > n and self.model.prefill_gemm != "hipblaslt":
+            # prefill rows ran: fetch the hand-written GEMM's error word with the tokens'
+            # own sync (a cross-workgroup wait that timed out - outputs are still exact, the
+            # workgroup recomputed; it signals a GPU shared with other work) - ADVICE r3
+            ops.prefill_gemm_error_to(self._err_host)
+        out = toks[:n].cpu().numpy()
+        if self.is_cuda and int(self._err_host[0]) != self.kernel_error:
+            self.kernel_error = int(self._err_host[0])
+            print(f"[model_runner] prefill GEMM error word {self.kernel_error:#x}: a "
+                  "cross-workgroup wait timed out (tiles recomputed, outputs exact; the GPU "
+                  "is shared or oversubscribed)", flush=True)
+        return out
 
     def launchable(self, batch: Batch) -> bool:
         """Decode-only batches can be launched asynchronously (every sampler runs on the

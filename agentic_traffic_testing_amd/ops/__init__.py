@@ -511,22 +511,20 @@ def prefill_gemm_ok(x: torch.Tensor, w: torch.Tensor, mode: int = GEMM_PLAIN) ->
             and n % (128 if mode == GEMM_SILU else 256) == 0)
 
 
+_PG_SCHEDULES = {"hybrid": 0, "streamk": 1, "dp": 2, "splitk": 3}
+
+
 def prefill_gemm(x: torch.Tensor, w: torch.Tensor, mode: int = GEMM_PLAIN,
                  residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
                  xs: torch.Tensor | None = None, ws: torch.Tensor | None = None,
-                 schedule: str | None = None) -> torch.Tensor:
+                 schedule: str | None = None, bm: int = 0) -> torch.Tensor:
     """Hand-written CDNA4 prefill GEMM: ``x @ w.T`` (GEMM_PLAIN), ``residual += x @ w.T`` in
     place (GEMM_RESADD; returns ``residual``) or ``silu(x @ gate.T) * (x @ up.T)`` for
     ``w = [gate; up]`` (GEMM_SILU).  bf16 operands, or fp8: uint8 e4m3fn ``x`` / ``w`` with
     fp32 row scales ``xs`` [M, 1] / ``ws`` [rows of w] (applied in the epilogue).  fp32
-    accumulate, one rounding to bf16.  ``schedule`` overrides the configured tile schedule
-    (prefill_gemm_config) for this call only.  CPU tensors run the PyTorch reference of the op."""
-    if schedule is not None and x.is_cuda:
-        prefill_gemm_config(schedule)
-        try:
-            return prefill_gemm(x, w, mode, residual, out, xs, ws)
-        finally:
-            prefill_gemm_config(_PG_SCHEDULE)
+    accumulate, one rounding to bf16.  ``schedule`` (hybrid / streamk / dp / splitk) and ``bm``
+    (tile height 64 / 128 / 256; 0 = by row count) apply to this call only - nothing
+    process-wide changes.  CPU tensors run the PyTorch reference of the op."""
     n = w.shape[0] // 2 if mode == GEMM_SILU else w.shape[0]
     fp8 = x.dtype == torch.uint8
     if fp8 and (xs is None or ws is None):
@@ -548,34 +546,48 @@ def prefill_gemm(x: torch.Tensor, w: torch.Tensor, mode: int = GEMM_PLAIN,
             out.copy_(y)
             return out
         return y
+    sched = -1 if schedule is None else _PG_SCHEDULES[schedule]
     xs_ = xs.reshape(-1) if fp8 else None
     ws_ = ws.reshape(-1) if fp8 else None
     if mode == GEMM_RESADD:
-        _native().prefill_gemm(residual, x, w, residual, mode, xs_, ws_)
+        _native().prefill_gemm(residual, x, w, residual, mode, xs_, ws_, sched, bm)
         return residual
     if out is None:
         out = torch.empty(x.shape[0], n, dtype=torch.bfloat16, device=x.device)
-    _native().prefill_gemm(out, x, w, None, mode, xs_, ws_)
+    _native().prefill_gemm(out, x, w, None, mode, xs_, ws_, sched, bm)
     return out
 
 
-_PG_SCHEDULE = "hybrid"  # the configured (process-wide) schedule
+_PG_SCHEDULE = "hybrid"  # the configured (process-wide) default schedule
 
 
 def prefill_gemm_config(schedule: str = "hybrid", group_m: int = 4, ablate: int = 0) -> None:
-    """Tile schedule of the prefill GEMM: "hybrid" (data-parallel rounds + Stream-K
-    remainder), "streamk", "dp" or "splitk" (co-resident K slices of a few whole tiles with a
-    parallel reduction, where T * S fits the CUs); ``group_m`` M tiles per raster group; ``ablate``
-    (measurement only, bf16 plain GEMMs): 1 no MFMA, 2 no LDS-DMA, 3 no ds_read."""
+    """Process-wide defaults of the prefill GEMM: schedule "hybrid" (data-parallel rounds +
+    Stream-K remainder), "streamk", "dp" or "splitk" (co-resident K slices of a few whole
+    tiles with a parallel reduction, where T * S fits the CUs); ``group_m`` M tiles per raster
+    group; ``ablate`` (measurement only, bf16 plain GEMMs): 1 no MFMA, 2 no LDS-DMA, 3 no
+    ds_read; 4 (tests): every cross-workgroup wait gives up at once (recompute fallback)."""
     global _PG_SCHEDULE
-    _native().prefill_gemm_config({"hybrid": 0, "streamk": 1, "dp": 2, "splitk": 3}[schedule],
-                                  group_m, ablate)
+    _native().prefill_gemm_config(_PG_SCHEDULES[schedule], group_m, ablate)
     _PG_SCHEDULE = schedule
 
 
+def prefill_gemm_auto_bm(m: int) -> int:
+    """Tile height the library picks for m rows (fewest padding rows)."""
+    return int(_native().prefill_gemm_auto_bm(m))
+
+
 def prefill_gemm_error() -> int:
-    """Nonzero once a stream-K finisher of the prefill GEMM timed out waiting for a partial."""
+    """Nonzero once a cross-workgroup wait of the prefill GEMM timed out (bit 1 stream-K,
+    bit 2 split-K); bit 4 says the waiting workgroup recomputed its tile itself, so the
+    outputs are still exact."""
     return int(_native().prefill_gemm_error())
+
+
+def prefill_gemm_error_to(host: torch.Tensor) -> None:
+    """Enqueue a copy of the prefill GEMM's error word into ``host`` (pinned int32) on the
+    current stream; read it after the next synchronisation (no extra sync of its own)."""
+    _native().prefill_gemm_error_to(host)
 
 
 def _need_cuda(x, preshuffled):

@@ -311,9 +311,12 @@ void skinny_gemm(at::Tensor y, const at::Tensor& x, const at::Tensor& w,
 // uint8 (e4m3fn) a / w with fp32 row scales xs [M, 1] / ws [rows of w].
 void prefill_gemm(at::Tensor c, const at::Tensor& a, const at::Tensor& w,
                   const c10::optional<at::Tensor>& residual, int64_t mode,
-                  const c10::optional<at::Tensor>& xs, const c10::optional<at::Tensor>& ws) {
+                  const c10::optional<at::Tensor>& xs, const c10::optional<at::Tensor>& ws,
+                  int64_t schedule, int64_t bm) {
   check_dev(a, "a");
   TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && c.dim() == 2, "prefill_gemm: 2-D operands");
+  TORCH_CHECK(schedule >= -1 && schedule <= 3 && (bm == 0 || bm == 64 || bm == 128 || bm == 256),
+              "prefill_gemm: schedule -1..3, bm 0 / 64 / 128 / 256");
   const bool fp8 = a.scalar_type() == at::kByte;
   TORCH_CHECK(c.scalar_type() == at::kBFloat16 && w.scalar_type() == a.scalar_type() &&
                   (fp8 || a.scalar_type() == at::kBFloat16),
@@ -345,11 +348,18 @@ void prefill_gemm(at::Tensor c, const at::Tensor& a, const at::Tensor& w,
   const at::DeviceGuard g(a.device());
   check_rc(atta_prefill_gemm(c.data_ptr(), a.data_ptr(), w.data_ptr(), r, a.size(0), n, a.size(1),
                              a.stride(0), w.stride(0), c.stride(0), rs, mode, fp8 ? 1 : 0, xsp,
-                             wsp, cur_stream()),
+                             wsp, static_cast<int>(schedule), static_cast<int>(bm), cur_stream()),
            "prefill_gemm");
 }
 
 int64_t prefill_gemm_error() { return atta_prefill_gemm_error(); }
+void prefill_gemm_error_to(at::Tensor host) {
+  TORCH_CHECK(host.device().is_cpu() && host.is_pinned() && host.scalar_type() == at::kInt &&
+                  host.numel() >= 1,
+              "prefill_gemm_error_to: a pinned int32 host tensor");
+  check_rc(atta_prefill_gemm_error_async(host.data_ptr(), cur_stream()), "prefill_gemm_error_to");
+}
+int64_t prefill_gemm_auto_bm(int64_t m) { return atta_prefill_gemm_auto_bm(static_cast<int>(m)); }
 void prefill_gemm_config(int64_t schedule, int64_t group_m, int64_t ablate) {
   check_rc(atta_prefill_gemm_config(static_cast<int>(schedule), static_cast<int>(group_m),
                                     static_cast<int>(ablate)),
@@ -831,8 +841,10 @@ TORCH_LIBRARY(atta, m) {
   m.def("sample_finalize(Tensor(a!) tokens, Tensor keys, int n_tiles) -> ()");
   m.def("skinny_gemm(Tensor(a!) y, Tensor x, Tensor w, Tensor? residual, int waves, "
         "bool preshuffled=False, Tensor? w_scale=None, int ksplit=1) -> ()");
-  m.def("prefill_gemm(Tensor(a!) c, Tensor a, Tensor w, Tensor? residual, int mode, Tensor? xs=None, Tensor? ws=None) -> ()");
+  m.def("prefill_gemm(Tensor(a!) c, Tensor a, Tensor w, Tensor? residual, int mode, Tensor? xs=None, Tensor? ws=None, int schedule=-1, int bm=0) -> ()");
+  m.def("prefill_gemm_auto_bm(int m) -> int", &prefill_gemm_auto_bm);
   m.def("prefill_gemm_error() -> int", &prefill_gemm_error);
+  m.def("prefill_gemm_error_to(Tensor(a!) host) -> ()", &prefill_gemm_error_to);
   m.def("prefill_gemm_config(int schedule, int group_m, int ablate=0) -> ()", &prefill_gemm_config);
   m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rms_norm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");

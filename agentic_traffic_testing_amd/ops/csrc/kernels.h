@@ -171,9 +171,13 @@ void atta_set_decode_step_trace(void* trace, void* stats);
 
 // Prefill GEMM (prefill_gemm.hip): c[M, N] = a[M, K] . w[N, K]^T; mode 0 plain, 1 c = res +
 // a.w^T (res may alias c), 2 c = silu(a.gate^T) * (a.up^T) with w = [gate; up].  fp8: a / w are
-// e4m3fn bytes with fp32 row scales xs [M] / wsc [rows of w]; else bf16.
+// e4m3fn bytes with fp32 row scales xs [M] / wsc [rows of w]; else bf16.  schedule -1 = the
+// configured default (atta_prefill_gemm_config), else 0-3; bm 0 = auto, else 64 / 128 / 256.
 int atta_prefill_gemm(void* c, const void* a, const void* w, const void* res, int M, int N,
                       int K, int64_t lda, int64_t ldw, int64_t ldc, int64_t ldres, int mode,
-                      int fp8, const float* xs, const float* wsc, hipStream_t stream);
+                      int fp8, const float* xs, const float* wsc, int schedule, int bm,
+                      hipStream_t stream);
+int atta_prefill_gemm_auto_bm(int M);
 int atta_prefill_gemm_error();
+int atta_prefill_gemm_error_async(void* host, hipStream_t stream);
 int atta_prefill_gemm_config(int schedule, int group_m, int ablate);

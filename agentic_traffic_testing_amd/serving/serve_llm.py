@@ -148,6 +148,12 @@ async def handle_health(request: web.Request) -> web.Response:
     if st.aengine is not None and (not st.aengine.alive or st.aengine.stalled(st.s.watchdog_s)):
         return web.json_response({"status": "unhealthy", "reason": "engine loop stalled"},
                                  status=503)
+    # kernel error word (prefill GEMM wait timed out -> tiles recomputed, outputs exact): the
+    # GPU is shared or oversubscribed; still serving, so 200 with the reason attached
+    err = getattr(getattr(st.engine, "runner", None), "kernel_error", 0) if st.engine else 0
+    if err:
+        return web.json_response({"status": "ok", "degraded": True,
+                                  "kernel_error_word": int(err)})
     return web.json_response({"status": "ok"})
 
 
@@ -405,6 +411,10 @@ def build_config(args):
         kw["device"] = args.device
     if getattr(args, "quantization", None):
         kw["quantization"] = args.quantization
+    if getattr(args, "burst_window_ms", None) is not None:
+        kw["burst_window_ms"] = args.burst_window_ms
+    if getattr(args, "burst_gap_ms", None) is not None:
+        kw["burst_gap_ms"] = args.burst_gap_ms
     return EngineConfig.from_env(**kw)
 
 
@@ -485,6 +495,11 @@ def make_parser() -> argparse.ArgumentParser:
     p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--load-format", default="auto", choices=["auto", "dummy", "safetensors"])
     p.add_argument("--device", default=None)
+    p.add_argument("--burst-window-ms", type=float, default=None,
+                   help="burst-aware admission: hold an announced fan-out (x-fanout) up to this "
+                        "long for its siblings (0 = FIFO admission, like vLLM)")
+    p.add_argument("--burst-gap-ms", type=float, default=None,
+                   help="... closing early once no sibling arrived for this long")
     p.add_argument("--config", default=None,
                    help="YAML file of EngineConfig keys (e.g. llm/config/llama-3.1-8b.yaml); "
                         "explicit flags win")
@@ -525,6 +540,10 @@ def _tp_worker_rank(args) -> bool:
 
 
 def main(argv=None) -> None:
+    # the host driver only supports dmabuf IPC: without this, RCCL and the IPC all-reduce's
+    # hipIpcGetMemHandle fail for TP > 1 (set before anything initialises HIP; compose and
+    # the Dockerfile set it too, a bare `python -m llm.serve_llm` must not depend on them)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     args = apply_config_file(make_parser().parse_args(argv))
     if args.data_parallel_size and args.data_parallel_size > 1:
         from ..parallel import dp_router

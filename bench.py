@@ -108,6 +108,9 @@ def parse_args(argv=None):
                     help="--via http workload: the /task fan-out (headline), the AgentVerse "
                          "loop (POST /agentverse, config 4) or multi-turn agents through the "
                          "OpenAI-compatible proxy (config 5's MCP-Universe path)")
+    ap.add_argument("--arrival-skew-ms", type=float, default=0.0,
+                    help="--via http: Agent A sends fan-out worker i's request i * ms late "
+                         "(arrival skew, e.g. netem jitter between the agents and the backend)")
     ap.add_argument("--max-tokens-limit", type=int, default=0,
                     help="--via http: clamp every LLM call's max_tokens (0 = off)")
     ap.add_argument("--via", choices=["engine", "http"], default="engine",
@@ -240,6 +243,17 @@ def main_dp(a, world: int):
             f"replay+sync {rt['graph_run'] / g * 1e3:.3f} ms")
     tokens = sum(r.completion_tokens for r in results)
     ttfts = [t for r in results for t in r.ttfts]
+    # TTFT by phase of the episode: rows actually prefilled (prompt - prefix-cache hits) and
+    # the median TTFT of the phase's requests
+    by_phase = {}
+    for r in results:
+        for name, pt, ct, tt in r.phases:
+            d = by_phase.setdefault(name, {"rows": [], "ttft": []})
+            d["rows"].append(pt - ct)
+            d["ttft"].extend(tt)
+    ttft_phases = {k: {"prefill_rows": int(statistics.median(v["rows"])),
+                       "p50_ttft_ms": round(statistics.median(v["ttft"]) * 1e3, 2)}
+                   for k, v in by_phase.items()}
     lat = [t for r in results for t in r.latencies]
     per_rank = [round(tokens / elapsed, 2)]
     if dist:
@@ -288,6 +302,7 @@ def main_dp(a, world: int):
             "p50_ttft_s": round(p50, 4) if p50 is not None else None,
             "p95_ttft_s": round(p95, 4) if p95 is not None else None,
             "p50_latency_s": round(statistics.median(lat), 3) if lat else None,
+            "ttft_by_phase": ttft_phases,
             "requests_per_step_per_gpu": 2 + a.fanout,
             "completion_tokens": int(tokens),
             "init_s": round(init_s, 1),
@@ -307,7 +322,8 @@ def _finish_http(a, eng, world, rank, dist, init_s, cfg, log):
         dist.barrier()
     _sync(a)
     r = run_e2e(eng, a.steps, a.warmup, fanout=a.fanout, max_tokens=a.max_tokens, log=log,
-                workload=a.workload, max_tokens_limit=a.max_tokens_limit)
+                workload=a.workload, max_tokens_limit=a.max_tokens_limit,
+                arrival_skew_ms=a.arrival_skew_ms)
     _sync(a)
     elapsed, tokens = r["seconds"], r["tokens"]
     per_rank = [round(r["tokens_per_s"], 2)]
@@ -341,7 +357,8 @@ def _finish_http(a, eng, world, rank, dist, init_s, cfg, log):
             "p95_ttft_s": round(p95, 4) if p95 is not None else None,
             "llm_calls": r["calls"], "llm_calls_per_workflow": r["calls_per_workflow"],
             "peak_inflight": r["peak_inflight"], "bursts_coalesced": r["bursts_coalesced"],
-            "ttft_breakdown": r.get("ttft_breakdown"),
+            "ttft_breakdown": r.get("ttft_breakdown"), "arrival_skew_ms": a.arrival_skew_ms,
+            "burst_window_ms": cfg.burst_window_ms, "burst_gap_ms": cfg.burst_gap_ms,
             "completion_tokens": int(tokens),
             "per_task_s": r["per_task_s"], "init_s": round(init_s, 1)}), flush=True)
     if dist:

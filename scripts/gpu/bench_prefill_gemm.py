@@ -8,6 +8,8 @@ columns).  The gate_up rows compare the fused SiLU-mul GEMM against hipBLASLt ga
 the silu_and_mul kernel (what the prefill path runs without it).
 
     python scripts/gpu/bench_prefill_gemm.py --m 512 1300 2600 > profiles/r3_prefill_gemm_ab.txt
+    python scripts/gpu/bench_prefill_gemm.py --m 73 382 --bm 64 128 256 \
+        --schedules hybrid splitk        # tile-height x schedule sweep, interleaved rounds
 """
 from __future__ import annotations
 
@@ -50,7 +52,14 @@ def main():
                     help="e4m3fn operands with row scales: ours vs hipBLASLt torch._scaled_mm")
     ap.add_argument("--schedule", default="hybrid", choices=["hybrid", "streamk", "dp", "splitk"])
     ap.add_argument("--group-m", type=int, default=4)
+    ap.add_argument("--bm", type=int, nargs="+", default=[0],
+                    help="tile heights to sweep (0 = the library's pick)")
+    ap.add_argument("--schedules", nargs="+", default=None,
+                    help="schedules to sweep per call (default: --schedule)")
+    ap.add_argument("--rounds", type=int, default=3,
+                    help="interleaved rounds of all variants; the median is reported")
     args = ap.parse_args()
+    scheds = args.schedules or [args.schedule]
     ops.prefill_gemm_config(args.schedule, args.group_m)
     dev = "cuda"
     print(f"# prefill GEMM A/B ({'fp8 e4m3fn, row scales' if args.fp8 else 'bf16'}), "
@@ -60,8 +69,10 @@ def main():
     for name, (n, k, mode) in SHAPES.items():
         if args.only and args.only not in name:
             continue
+        # enough copies that the rotation (>= 768 MB) never fits the 256 MB Infinity Cache
+        copies = max(args.copies, int(768e6 / (n * k * 2)) + 1)
         ws = [(torch.rand(n, k, device=dev) * 2 - 1).to(torch.bfloat16) / k ** 0.5
-              for _ in range(args.copies)]
+              for _ in range(copies)]
         if args.fp8:
             qs = [ops.quant_rows_fp8(w) for w in ws]
             ws = [q for q, _ in qs]
@@ -75,13 +86,15 @@ def main():
             out = torch.empty(m, nout, device=dev, dtype=torch.bfloat16)
             flops = 2.0 * m * n * k
 
-            def ours(i):
-                w = ws[i % len(ws)]
-                kw = dict(xs=xs, ws=wsc[i % len(ws)]) if args.fp8 else {}
-                if mode == ops.GEMM_RESADD:
-                    ops.prefill_gemm(x, w, mode, residual=res, **kw)
-                else:
-                    ops.prefill_gemm(x, w, mode, out=out, **kw)
+            def make(bm, sched):
+                def ours(i):
+                    w = ws[i % len(ws)]
+                    kw = dict(xs=xs, ws=wsc[i % len(ws)]) if args.fp8 else {}
+                    if mode == ops.GEMM_RESADD:
+                        ops.prefill_gemm(x, w, mode, residual=res, schedule=sched, bm=bm, **kw)
+                    else:
+                        ops.prefill_gemm(x, w, mode, out=out, schedule=sched, bm=bm, **kw)
+                return ours
 
             def lin(i):
                 w = ws[i % len(ws)]
@@ -100,23 +113,33 @@ def main():
                 else:
                     lin(i)
 
-            # numerics spot check against hipBLASLt (fp32 accumulate both)
+            # numerics spot check against hipBLASLt (fp32 accumulate both), every variant
             ref = lin(0).float()
-            kw = dict(xs=xs, ws=wsc[0]) if args.fp8 else {}
             if mode == ops.GEMM_SILU:
                 ref = torch.nn.functional.silu(ref[:, :nout]) * ref[:, nout:]
-                got = ops.prefill_gemm(x, ws[0], mode, **kw).float()
-            else:
-                got = ops.prefill_gemm(x, ws[0], **kw).float()
-            err = ((got - ref).abs().max() / ref.abs().max()).item()
-            t_ours = timed(ours, args.iters)
-            t_blas = timed(blas, args.iters)
-            print(f"{name:13s} M={m:5d} N={n:6d} K={k:6d} | atta {t_ours:8.1f} us "
-                  f"{flops / t_ours / 1e6:7.0f} TF | hipBLASLt {t_blas:8.1f} us "
-                  f"{flops / t_blas / 1e6:7.0f} TF | speedup {t_blas / t_ours:5.2f}x "
-                  f"| rel err {err:.2e}", flush=True)
+            variants = [(bm, sc) for bm in args.bm for sc in scheds]
+            err = 0.0
+            for bm, sc in variants:
+                kw = dict(xs=xs, ws=wsc[0]) if args.fp8 else {}
+                got = ops.prefill_gemm(x, ws[0], mode if mode == ops.GEMM_SILU else 0,
+                                       schedule=sc, bm=bm, **kw).float()
+                err = max(err, ((got - ref).abs().max() / ref.abs().max()).item())
+            times = {v: [] for v in variants}
+            tb = []
+            for _ in range(args.rounds):
+                tb.append(timed(blas, args.iters))
+                for v in variants:
+                    times[v].append(timed(make(*v), args.iters))
+            t_blas = sorted(tb)[len(tb) // 2]
+            med = {v: sorted(t)[len(t) // 2] for v, t in times.items()}
+            best = min(med, key=med.get)
+            cols = " ".join(f"{bm or 'auto'}/{sc}:{med[(bm, sc)]:7.1f}" for bm, sc in variants)
+            print(f"{name:13s} M={m:5d} N={n:6d} K={k:6d} | hipBLASLt {t_blas:8.1f} us "
+                  f"{flops / t_blas / 1e6:6.0f} TF | {cols} | best {best[0] or 'auto'}/{best[1]} "
+                  f"{med[best]:7.1f} us {flops / med[best] / 1e6:6.0f} TF "
+                  f"{t_blas / med[best]:5.2f}x | rel err {err:.2e}", flush=True)
         del ws
-    assert ops.prefill_gemm_error() == 0, "stream-K finisher timed out"
+    assert ops.prefill_gemm_error() == 0, "a cross-workgroup wait timed out"
 
 
 if __name__ == "__main__":

@@ -16,11 +16,12 @@ def _engine():
                                   use_graphs=False))
 
 
-def _run(window_s, plan):
-    """plan: [(delay_s, request_id, burst)] submitted in order; returns (steps, ttfts)."""
+def _run(window_s, plan, gap_s=10.0):
+    """plan: [(delay_s, request_id, burst)] submitted in order; returns (steps, ttfts).
+    gap_s: the early-close gap (default: large, i.e. the window alone decides)."""
     steps = []
     ae = AsyncEngine(_engine(), on_step=lambda st, dt: steps.append(st),
-                     burst_window_s=window_s).start()
+                     burst_window_s=window_s, burst_gap_s=gap_s).start()
     sp = SamplingParams(temperature=0.0, max_tokens=2, ignore_eos=True)
     ttft = {}
 
@@ -76,3 +77,84 @@ def test_straggler_after_deadline_not_held_again():
     plan = [(0.0, "e0", ("task-5", 2)), (0.3, "e1", ("task-5", 2))]
     steps, ttft, ae = _run(0.05, plan)
     assert ttft["e1"] < 0.04, ttft  # no second 50 ms window
+
+
+# ---- deterministic policy tests on _take_pending (no engine thread, controlled clock) -----
+class _FakeEngine:
+    class cfg:
+        burst_window_ms = 10.0
+        burst_gap_ms = 4.0
+
+    def __init__(self):
+        self.admitted = []
+
+    def add_request(self, rid, ids, sp, arrival_time=None):
+        self.admitted.append(rid)
+
+
+def _policy(window_s=0.010, gap_s=0.004):
+    eng = _FakeEngine()
+    return AsyncEngine(eng, burst_window_s=window_s, burst_gap_s=gap_s), eng
+
+
+def _arrive(ae, rid, t, key="task", size=5):
+    ae._pending.append((rid, [1, 2], None, t, (key, size)))
+
+
+def test_skewed_arrivals_close_window_early():
+    """Arrival skew larger than the window (netem-like, 30 ms apart): the lone early request
+    waits only the 4 ms gap, not the 10 ms window, and every later sibling goes at once."""
+    ae, eng = _policy()
+    t0 = 100.0
+    _arrive(ae, "s0", t0)
+    assert ae._take_pending(t0) == t0 + 0.004  # held, deadline = last arrival + gap
+    assert eng.admitted == []
+    ae._take_pending(t0 + 0.0041)
+    assert eng.admitted == ["s0"]
+    for i in range(1, 5):  # stragglers of the flushed burst: admitted on arrival
+        t = t0 + 0.030 * i
+        _arrive(ae, f"s{i}", t)
+        ae._take_pending(t)
+        assert eng.admitted[-1] == f"s{i}"
+    assert not ae._held and not ae._flushed
+
+
+def test_lan_burst_coalesces_within_gap():
+    """A LAN fan-out (siblings 0.5-1 ms apart) is held to the last sibling and admitted as
+    one group; each arrival pushes the gap deadline, the window caps it."""
+    ae, eng = _policy()
+    t0 = 5.0
+    for i in range(5):
+        _arrive(ae, f"l{i}", t0 + 0.0008 * i)
+        dl = ae._take_pending(t0 + 0.0008 * i)
+        if i < 4:
+            assert eng.admitted == [] and abs(dl - (t0 + 0.0008 * i + 0.004)) < 1e-9
+    assert eng.admitted == [f"l{i}" for i in range(5)]
+    assert ae.bursts_coalesced == 1
+
+
+def test_window_caps_a_slow_trickle():
+    ae, eng = _policy(window_s=0.010, gap_s=0.004)
+    t0 = 1.0
+    for i in range(4):  # 3 ms apart: the gap never expires, the 10 ms window does
+        _arrive(ae, f"w{i}", t0 + 0.003 * i)
+        ae._take_pending(t0 + 0.003 * i)
+    assert eng.admitted == []
+    assert ae._take_pending(t0 + 0.0095) == t0 + 0.010
+    ae._take_pending(t0 + 0.0101)
+    assert eng.admitted == ["w0", "w1", "w2", "w3"]
+
+
+def test_flushed_records_expire_without_stragglers():
+    """A burst flushed at its deadline whose siblings never come must not leak its record
+    (the dict grew without bound in a long-running server)."""
+    ae, eng = _policy()
+    for k in range(50):
+        t = 10.0 + k * 0.1
+        _arrive(ae, f"f{k}", t, key=f"task-{k}", size=3)
+        ae._take_pending(t)
+        ae._take_pending(t + 0.005)  # gap expired: flushed with 2 stragglers expected
+    assert len(eng.admitted) == 50
+    assert 0 < len(ae._flushed) <= 50
+    ae._take_pending(10.0 + 50 * 0.1 + ae.FLUSHED_TTL_S + 0.01)
+    assert ae._flushed == {}

@@ -153,60 +153,106 @@ def test_prefill_gemm_fp8_vs_fp32(mode, mnk):
     assert ops.prefill_gemm_error() == 0
 
 
-@pytest.fixture
-def splitk_schedule():
-    ops.prefill_gemm_config("splitk")
-    yield
-    ops.prefill_gemm_config("hybrid")
-
-
 @pytest.mark.gpu
+@pytest.mark.parametrize("sched", ["hybrid", "streamk", "dp", "splitk"])
+@pytest.mark.parametrize("bm", [64, 128, 256])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-@pytest.mark.parametrize("mnk", [(400, 4096, 14336), (77, 512, 4096), (512, 1024, 2048),
-                                 (300, 256, 512)])
-def test_prefill_gemm_splitk_vs_fp32(splitk_schedule, mode, mnk):
-    """Split-K schedule (co-resident K slices, each workgroup reducing its own row fragments
-    over every slice): the fan-out burst's down_proj shape (400 x 4096 x 14336: 32 tiles x 8
-    slices), ragged M, the smallest slice (8 phases)."""
+@pytest.mark.parametrize("mnk", [(73, 1024, 4096), (382, 768, 2048), (700, 512, 1024)])
+def test_prefill_gemm_tiles_schedules_vs_fp32(sched, bm, mode, mnk):
+    """Every tile height (64 / 128 / 256 rows) under every schedule, chosen per call: the
+    planning-call (73 rows) and fan-out-burst (382 rows) shapes, ragged M in every tile."""
     assert ops.native_available(), ops._load_error
     M, N, K = mnk
-    torch.manual_seed(M + N + K + mode)
+    torch.manual_seed(M + N + K + mode + bm)
     x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
     rows = 2 * N if mode == ops.GEMM_SILU else N
     w = (torch.randn(rows, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
+    kw = dict(schedule=sched, bm=bm)
     if mode == ops.GEMM_RESADD:
         r = torch.randn(M, N, device="cuda").to(torch.bfloat16)
         exp = _ref(x, w, mode, r)
-        got = ops.prefill_gemm(x, w, mode, residual=r)
+        got = ops.prefill_gemm(x, w, mode, residual=r, **kw)
     else:
         exp = _ref(x, w, mode)
-        got = ops.prefill_gemm(x, w, mode)
+        got = ops.prefill_gemm(x, w, mode, **kw)
+        # deterministic: partials are summed in a fixed order whoever finishes last
+        assert torch.equal(ops.prefill_gemm(x, w, mode, **kw), got)
     torch.cuda.synchronize()
     _check(got, exp, K)
     assert ops.prefill_gemm_error() == 0
-    # deterministic: the slices are summed in slice order whichever workgroup finishes last
-    if mode != ops.GEMM_RESADD:
-        again = ops.prefill_gemm(x, w, mode)
-        assert torch.equal(again, got)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("bm", [64, 128, 256])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_prefill_gemm_fp8_splitk_vs_fp32(splitk_schedule, mode):
+def test_prefill_gemm_fp8_tiles_vs_fp32(bm, mode):
     assert ops.native_available(), ops._load_error
-    M, N, K = 400, 1024, 4096
-    torch.manual_seed(5 + mode)
+    M, N, K = 382, 1024, 4096
+    torch.manual_seed(5 + mode + bm)
     rows = 2 * N if mode == ops.GEMM_SILU else N
     xq, xs = _q8(torch.randn(M, K, device="cuda"))
     wq, ws = _q8(torch.randn(rows, K, device="cuda") / K ** 0.5)
     ws = ws.reshape(-1).contiguous()
-    if mode == ops.GEMM_RESADD:
-        r = torch.randn(M, N, device="cuda").to(torch.bfloat16)
-        exp = _ref8(xq, xs, wq, ws, mode, r)
-        got = ops.prefill_gemm(xq, wq, mode, residual=r, xs=xs, ws=ws)
-    else:
-        exp = _ref8(xq, xs, wq, ws, mode)
-        got = ops.prefill_gemm(xq, wq, mode, xs=xs, ws=ws)
-    torch.cuda.synchronize()
-    _check(got, exp, K)
+    for sched in ("hybrid", "splitk"):
+        if mode == ops.GEMM_RESADD:
+            r = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+            exp = _ref8(xq, xs, wq, ws, mode, r)
+            got = ops.prefill_gemm(xq, wq, mode, residual=r, xs=xs, ws=ws, schedule=sched, bm=bm)
+        else:
+            exp = _ref8(xq, xs, wq, ws, mode)
+            got = ops.prefill_gemm(xq, wq, mode, xs=xs, ws=ws, schedule=sched, bm=bm)
+        torch.cuda.synchronize()
+        _check(got, exp, K)
     assert ops.prefill_gemm_error() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sched", ["streamk", "splitk"])
+@pytest.mark.parametrize("mode", [0, 2])
+def test_prefill_gemm_timed_out_wait_recomputes(sched, mode):
+    """A cross-workgroup wait that gives up (forced: ablate=4 makes every wait time out at
+    once) recomputes the tile over the whole K range: the output stays exact and the error
+    word says so (bit 4), instead of reading partials nobody wrote."""
+    assert ops.native_available(), ops._load_error
+    M, N, K = 300, 1024, 4096
+    torch.manual_seed(13 + mode)
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    rows = 2 * N if mode == ops.GEMM_SILU else N
+    w = (torch.randn(rows, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
+    exp = _ref(x, w, mode)
+    ops.prefill_gemm_config("hybrid", ablate=4)
+    try:
+        got = ops.prefill_gemm(x, w, mode, schedule=sched, bm=128)
+        torch.cuda.synchronize()
+    finally:
+        ops.prefill_gemm_config("hybrid")
+    _check(got, exp, K)
+    assert ops.prefill_gemm_error() & 4
+    # the protocol state is re-armed: a normal call afterwards is exact and times out nowhere
+    got2 = ops.prefill_gemm(x, w, mode, schedule=sched, bm=128)
+    torch.cuda.synchronize()
+    _check(got2, exp, K)
+
+
+def test_prefill_gemm_per_call_schedule_keeps_process_config(monkeypatch):
+    """schedule= / bm= travel with the call; the process-wide configuration is never touched
+    (the old override reset group_m / ablate and left 'splitk' behind)."""
+    calls = []
+
+    class Fake:
+        def prefill_gemm(self, *a):
+            calls.append(("gemm",) + a[-2:])
+
+        def prefill_gemm_config(self, *a):
+            calls.append(("config",) + a)
+
+    monkeypatch.setattr(ops, "_native", lambda: Fake())
+    before = ops._PG_SCHEDULE
+    x = torch.zeros(4, 64, dtype=torch.bfloat16, device="meta")
+    w = torch.zeros(256, 64, dtype=torch.bfloat16, device="meta")
+    monkeypatch.setattr(torch.Tensor, "is_cuda", property(lambda self: True))
+    ops.prefill_gemm(x, w, out=torch.zeros(4, 256, dtype=torch.bfloat16, device="meta"),
+                     schedule="splitk", bm=128)
+    ops.prefill_gemm(x, w, out=torch.zeros(4, 256, dtype=torch.bfloat16, device="meta"))
+    assert calls == [("gemm", 3, 128), ("gemm", -1, 0)]
+    assert ops._PG_SCHEDULE == before
