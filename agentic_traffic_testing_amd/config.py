@@ -205,9 +205,6 @@ class EngineConfig:
     long_prefill_token_threshold: int = 0
     # fused native decode path (GEMV kernels) when available
     fused_decode: bool = True
-    # whole decode step as ONE persistent launch (ops/csrc/decode_step.hip): TP = 1 bf16
-    # models whose shapes it covers, decode batches <= decode_small_batch_max rows
-    decode_megakernel: bool = False
     # burst-aware admission (engine/async_engine.py): requests that announce their fan-out
     # (X-Task-ID + x-fanout headers) are held up to this long for their siblings so the
     # burst shares one prefill; 0 disables.  Requests without the headers are never held.

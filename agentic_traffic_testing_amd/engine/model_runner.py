@@ -199,11 +199,6 @@ class ModelRunner:
             "part_out": self.part_out, "part_lse": self.part_lse,
             "max_parts": self.max_parts, "part_tokens": self.part_tokens,
         }
-        self.mk_sync = None
-        if self.is_cuda and cfg.decode_megakernel and self.model.megakernel_ok() \
-                and cfg.block_size == 16:
-            self.ws["x"] = torch.empty(self.max_seqs, H, dtype=dt, device=dev)
-            self.mk_sync = ops.decode_step_sync(self.mcfg.num_layers, dev)
         del H
         # the fused decode attention combines <= 64 partitions in-kernel (<= 16k tokens at
         # 256-token partitions); longer contexts use the two-kernel split-K path
@@ -350,12 +345,6 @@ class ModelRunner:
                         tile_qoff=v["tile_qoff"], logits_idx=v["logits_idx"],
                         num_decode=num_decode, num_tiles=num_tiles)
 
-    def _mk_ok(self, rows: int) -> bool:
-        """Persistent decode step for this decode batch: enabled, shapes covered, <= 16 rows
-        and the batch uses 128-token attention partitions (the kernel's partition size)."""
-        return (self.mk_sync is not None and rows <= 16 and self._small(rows)
-                and self.part_tokens_small == 128)
-
     def _small(self, batch_size: int) -> bool:
         return (0 < batch_size <= self.cfg.decode_small_batch_max
                 and self.part_tokens_small != self.part_tokens)
@@ -377,14 +366,6 @@ class ModelRunner:
         T = v["input_ids"].shape[0]
         if (self.fused_decode and md.num_tiles == 0
                 and md.num_decode == T and m.decode_fusable(T)):
-            if not special and self._mk_ok(T):
-                # the whole step in one persistent launch (ops/csrc/decode_step.hip)
-                return ops.decode_step(m.mk_layers, m.lm_head_ps, m.embed, self.k_cache,
-                                       self.v_cache, md, v["input_ids"], self.ws["tokens"],
-                                       v["feed_prev"], m.cos_sin, v["temperature"], v["seeds"],
-                                       v["steps"], self.ws, self.mk_sync, m.n_heads,
-                                       m.n_kv_heads, m.inter, self.mcfg.rms_norm_eps, m.scale,
-                                       num_parts)
             ws = self._ws_for(T)
             # grid over this step's partition bucket only (num_parts covers every row, in
             # the partition size of this batch size: parts_bucket)

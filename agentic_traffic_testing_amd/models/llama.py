@@ -106,7 +106,6 @@ class LlamaModel:
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
         self.layers: list[LayerWeights] = []
         self.lm_head_ps = None
-        self.mk_layers = None
         self.embed = None
         self.norm = None
         self.lm_head = None
@@ -266,21 +265,8 @@ class LlamaModel:
             L.gate_up_ps = ops.preshuffle(L.gate_up, "silu")
             L.down_ps = ops.preshuffle(L.down)
         self.lm_head_ps = ops.preshuffle(self.lm_head)
-        # address table of the pre-shuffled layer weights for the persistent decode step
-        self.mk_layers = torch.tensor(
-            [[l.qkv_ps.data_ptr(), l.o_ps.data_ptr(), l.gate_up_ps.data_ptr(),
-              l.down_ps.data_ptr()] for l in self.layers], dtype=torch.int64, device=self.device)
         torch.cuda.synchronize(self.device)
         return self
-
-    def megakernel_ok(self) -> bool:
-        """Shapes the persistent decode step (ops.decode_step) covers: TP = 1, bf16
-        pre-shuffled weights, K dims in 2048-wide wave chunks, GQA group 1 / 2 / 4."""
-        H, D = self.cfg.hidden_size, self.head_dim
-        return (self.device.type == "cuda" and self.tp_size == 1 and self.quant == ""
-                and self.dtype == torch.bfloat16 and getattr(self, "mk_layers", None) is not None
-                and self.lm_head_ps is not None and H % 2048 == 0 and self.inter % 2048 == 0
-                and (self.n_heads * D) % 2048 == 0 and D == 128 and self.g in (1, 2, 4))
 
     def decode_copy_bytes(self) -> int:
         """Bytes ``prepare_decode_weights`` adds (one copy of every decode GEMV weight)."""

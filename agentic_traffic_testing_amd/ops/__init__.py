@@ -732,99 +732,3 @@ def attention_decode_v2(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart
                                   block_tables, seq_kvlen, seq_qstart, num_seqs, max_parts,
                                   part_tokens, q.shape[1], k_cache.shape[1], scale)
     return out
-
-
-# ---- persistent decode step (ops/csrc/decode_step.hip) ------------------------------------
-def decode_step_sync(layers: int, device) -> torch.Tensor:
-    """Zeroed hand-off state of the persistent decode step: per-phase arrival counters (8
-    per-XCD shards), the final counter and the error word.  The kernel leaves it zeroed after
-    every complete launch, so one buffer serves every graph replay."""
-    return torch.zeros(int(_native().decode_step_sync_words(layers)), dtype=torch.int32,
-                       device=device)
-
-
-def decode_step_error(sync: torch.Tensor, layers: int) -> int:
-    """Error word of the persistent decode step (0 = every bounded wait succeeded; bits: 1 phase
-    poll, 2 ring FULL, 4 ring FREE, 8 LDS barrier).  Synchronises with the device."""
-    return int(sync[int(_native().decode_step_error_index(layers))].item())
-
-
-def set_decode_step_trace(trace: torch.Tensor | None = None, stats: torch.Tensor | None = None):
-    """Profiling of the persistent decode-step launches that follow (None: off): ``trace``
-    int64 [grid, 3 + 5 L, 2] wall-clock stamps (100 MHz) of every phase's begin (after its
-    poll) and end (before its arrival) per workgroup; ``stats`` int64 [grid, 4] shader cycles
-    of loader FREE waits, loader lifetime, wave-0 FULL waits and wave-0 poll waits."""
-    _native().set_decode_step_trace(trace, stats)
-
-
-def decode_step_grid() -> int:
-    return int(_native().decode_step_grid())
-
-
-def decode_step(layers_table: torch.Tensor, lm_head: torch.Tensor, embed: torch.Tensor,
-                k_cache: torch.Tensor, v_cache: torch.Tensor, md, input_ids: torch.Tensor,
-                prev_tokens: torch.Tensor, feed_prev: torch.Tensor, cos_sin: torch.Tensor,
-                temperature: torch.Tensor, seeds: torch.Tensor, steps: torch.Tensor, ws: dict,
-                sync: torch.Tensor, n_q_heads: int, n_kv_heads: int, inter: int, eps: float,
-                scale: float, max_parts: int) -> torch.Tensor:
-    """The whole decode step of a TP=1 16-bit model in ONE persistent launch (embedding ->
-    every layer -> LM head -> Gumbel-max sampler); tokens land in ws["tokens"][:M].
-
-    ``layers_table``: device int64 [L, 4] of the pre-shuffled qkv / o / gate_up / down weight
-    addresses; ``k_cache`` / ``v_cache``: the full [L, blocks, Hkv, 16, 128] / [L, blocks, Hkv,
-    128, 16] caches; ``md``: the step's AttnMeta (decode rows only, M = its row count).
-    Every tensor is checked here - the kernel indexes with these shapes unchecked."""
-    M = input_ids.shape[0]
-    L = layers_table.shape[0]
-    H = embed.shape[1]
-    V = lm_head.shape[0]
-    dev = embed.device
-    bf = embed.dtype
-    if not embed.is_cuda or bf != torch.bfloat16:
-        raise ValueError("decode_step: bf16 GPU model only")
-    if layers_table.dtype != torch.int64 or tuple(layers_table.shape) != (L, 4):
-        raise ValueError("decode_step: layers_table int64 [L, 4]")
-    if lm_head.shape[1] != H or lm_head.dtype != bf or not lm_head.is_contiguous():
-        raise ValueError("decode_step: lm_head [V, H] bf16")
-    if k_cache.dim() != 5 or k_cache.shape[0] != L or k_cache.shape[3] != 16 or \
-            k_cache.shape[4] != 128 or tuple(v_cache.shape) != (L, k_cache.shape[1],
-                                                               k_cache.shape[2], 128, 16):
-        raise ValueError("decode_step: paged caches [L, nb, Hkv, 16, 128] / [L, nb, Hkv, 128, 16]")
-    if k_cache.shape[2] != n_kv_heads or not (k_cache.is_contiguous() and v_cache.is_contiguous()):
-        raise ValueError("decode_step: cache heads / layout")
-    for name, t, dt, n in (("positions", md.positions, torch.int32, M),
-                           ("slot_mapping", md.slot_mapping, torch.int32, M),
-                           ("seq_kvlen", md.seq_kvlen, torch.int32, M),
-                           ("input_ids", input_ids, torch.int32, M),
-                           ("temperature", temperature, torch.float32, M),
-                           ("seeds", seeds, torch.int64, M), ("steps", steps, torch.int64, M),
-                           ("prev_tokens", prev_tokens, torch.int64, M),
-                           ("feed_prev", feed_prev, torch.int32, 1)):
-        if t.dtype != dt or t.numel() < n or not t.is_contiguous() or t.device != dev:
-            raise ValueError(f"decode_step: {name} must be contiguous {dt} >= {n} on {dev}")
-    bt = md.block_tables
-    if bt.dtype != torch.int32 or bt.dim() != 2 or bt.shape[0] < M or bt.stride(1) != 1:
-        raise ValueError("decode_step: block_tables int32 [S, W]")
-    if not 1 <= max_parts <= 64:
-        raise ValueError("decode_step: 1..64 attention partitions")
-    NQ = n_q_heads
-    x, q, attn, act = ws["x"], ws["q"], ws["attn"], ws["act"]
-    if x.shape[0] < M or x.shape[1] != H or q.numel() < M * NQ * 128 or \
-            attn.numel() < M * NQ * 128 or act.shape[0] < M or act.shape[1] != inter:
-        raise ValueError("decode_step: workspace shapes")
-    if ws["keys"].numel() < M * (V // 16) or ws["tokens"].numel() < M or \
-            ws["counters"].numel() < M * n_kv_heads or \
-            ws["part_out"].numel() < M * n_kv_heads * max_parts * 16 * 128 or \
-            ws["part_lse"].numel() < M * n_kv_heads * max_parts * 16:
-        raise ValueError("decode_step: workspace sizes")
-    if sync.numel() < int(_native().decode_step_sync_words(L)):
-        raise ValueError("decode_step: sync buffer too small")
-    ptrs = torch.tensor([t.data_ptr() for t in (
-        layers_table, lm_head, embed, k_cache, v_cache, input_ids, prev_tokens, feed_prev,
-        md.positions, md.slot_mapping, bt, md.seq_kvlen, cos_sin, temperature, seeds, steps,
-        x, q, attn, act, ws["part_out"], ws["part_lse"], ws["counters"], ws["keys"],
-        ws["tokens"], sync)], dtype=torch.int64)
-    layer_elems = k_cache[0].numel()
-    dims = [M, H, inter, V, L, NQ, n_kv_heads, bt.shape[1], max_parts, 16, layer_elems]
-    _native().decode_step(ptrs, dims, eps, scale, embed)
-    return ws["tokens"][:M]

@@ -682,69 +682,6 @@ void ar2_run(const at::Tensor& x, at::Tensor y, at::IntArrayRef bases, int64_t r
 }
 
 // ---- persistent decode step ----------------------------------------------------------------
-// ptrs: CPU int64 [26] of device addresses (order: ops.decode_step); dims: M, H, I, V, L, NQ,
-// NKV, bt_stride, max_parts, block_size, cache_layer_elems.  The Python side validates shapes
-// and keeps the tensors alive; this only forwards.
-void decode_step(const at::Tensor& ptrs, at::IntArrayRef dims, double eps, double scale,
-                 const at::Tensor& anchor) {
-  TORCH_CHECK(!ptrs.is_cuda() && ptrs.scalar_type() == at::kLong && ptrs.numel() == 26,
-              "decode_step: 26 CPU int64 pointers");
-  TORCH_CHECK(dims.size() == 11, "decode_step: 11 dims");
-  check_dev(anchor, "anchor");
-  const int64_t* a = ptrs.data_ptr<int64_t>();
-  auto P = [&](int i) { return reinterpret_cast<void*>(a[i]); };
-  DecodeStepArgs d{};
-  d.M = static_cast<int>(dims[0]);
-  d.H = static_cast<int>(dims[1]);
-  d.I = static_cast<int>(dims[2]);
-  d.V = static_cast<int>(dims[3]);
-  d.L = static_cast<int>(dims[4]);
-  d.NQ = static_cast<int>(dims[5]);
-  d.NKV = static_cast<int>(dims[6]);
-  d.bt_stride = static_cast<int>(dims[7]);
-  d.max_parts = static_cast<int>(dims[8]);
-  d.block_size = static_cast<int>(dims[9]);
-  d.cache_layer_elems = dims[10];
-  d.eps = static_cast<float>(eps);
-  d.scale = static_cast<float>(scale);
-  d.layers = P(0);
-  d.lm_head = P(1);
-  d.embed = P(2);
-  d.k_cache = P(3);
-  d.v_cache = P(4);
-  d.input_ids = static_cast<const int*>(P(5));
-  d.prev_tokens = static_cast<const int64_t*>(P(6));
-  d.feed_prev = static_cast<const int*>(P(7));
-  d.positions = static_cast<const int*>(P(8));
-  d.slots = static_cast<const int*>(P(9));
-  d.block_tables = static_cast<const int*>(P(10));
-  d.seq_kvlen = static_cast<const int*>(P(11));
-  d.cos_sin = static_cast<const float*>(P(12));
-  d.temperature = static_cast<const float*>(P(13));
-  d.seeds = static_cast<const int64_t*>(P(14));
-  d.steps = static_cast<const int64_t*>(P(15));
-  d.x = P(16);
-  d.q = P(17);
-  d.attn = P(18);
-  d.act = P(19);
-  d.part_out = static_cast<float*>(P(20));
-  d.part_lse = static_cast<float*>(P(21));
-  d.att_counters = static_cast<int*>(P(22));
-  d.keys = static_cast<unsigned long long*>(P(23));
-  d.tokens = static_cast<int64_t*>(P(24));
-  d.sync = static_cast<unsigned*>(P(25));
-  const at::DeviceGuard g(anchor.device());
-  check_rc(atta_decode_step(d, cur_stream()), "decode_step");
-}
-
-int64_t decode_step_sync_words(int64_t layers) {
-  return atta_decode_step_sync_words(static_cast<int>(layers));
-}
-int64_t decode_step_error_index(int64_t layers) {
-  return atta_decode_step_error_index(static_cast<int>(layers));
-}
-int64_t decode_step_grid() { return atta_decode_step_grid(); }
-
 // Node list of a captured hipGraph (torch.cuda.CUDAGraph(keep_graph=True).raw_cuda_graph()):
 // "kernel:<name> grid=x,y,z block=x" / "memcpy" / "memset" / "host" / ... in graph order -
 // evidence of what a captured decode step contains (scripts/gpu/graph_nodes.py).
@@ -784,24 +721,9 @@ std::vector<std::string> graph_nodes(int64_t graph) {
   return out;
 }
 
-void set_decode_step_trace(const c10::optional<at::Tensor>& trace,
-                           const c10::optional<at::Tensor>& stats) {
-  for (const auto* t : {&trace, &stats})
-    if (t->has_value())
-      TORCH_CHECK((*t)->is_cuda() && (*t)->scalar_type() == at::kLong && (*t)->is_contiguous(),
-                  "set_decode_step_trace: int64 cuda tensors");
-  atta_set_decode_step_trace(trace.has_value() ? trace->data_ptr() : nullptr,
-                             stats.has_value() ? stats->data_ptr() : nullptr);
-}
-
 }  // namespace
 
 TORCH_LIBRARY(atta, m) {
-  m.def("decode_step(Tensor ptrs, int[] dims, float eps, float scale, Tensor anchor) -> ()");
-  m.def("decode_step_sync_words(int layers) -> int", &decode_step_sync_words);
-  m.def("decode_step_error_index(int layers) -> int", &decode_step_error_index);
-  m.def("decode_step_grid() -> int", &decode_step_grid);
-  m.def("set_decode_step_trace(Tensor? trace, Tensor? stats) -> ()", &set_decode_step_trace);
   m.def("graph_nodes(int graph) -> str[]", &graph_nodes);
   m.def("ar_buffer_bytes(int max_elems, int elem_bytes) -> int", &ar_buffer_bytes);
   m.def("ar_alloc(int bytes, int device) -> int", &ar_alloc);
@@ -877,7 +799,6 @@ TORCH_LIBRARY_IMPL(atta, CUDA, m) {
   m.impl("ar_run", &ar_run);
   m.impl("ar2_run", &ar2_run);
   m.impl("ar_keymax", &ar_keymax);
-  m.impl("decode_step", &decode_step);
   m.impl("rms_norm", &rms_norm);
   m.impl("fused_add_rms_norm", &fused_add_rms_norm);
   m.impl("silu_and_mul", &silu_and_mul);

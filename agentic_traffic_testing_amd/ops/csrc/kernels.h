@@ -130,45 +130,6 @@ int atta_ar2_run(void* const* bases, int rank, int world, int64_t max_elems, con
                  void* y, const void* res, int64_t n, int dtype, hipStream_t stream);
 
 
-// ---- persistent decode step (decode_step.hip) --------------------------------------------
-struct DecodeStepArgs {
-  int M, H, I, V, L, NQ, NKV, bt_stride, max_parts, block_size;
-  float eps, scale;
-  const void* layers;  // device array [L] of {qkv, o, gate_up, down} pre-shuffled weight pointers
-  const void* lm_head;
-  const void* embed;
-  void* k_cache;
-  void* v_cache;
-  int64_t cache_layer_elems;
-  const int* input_ids;
-  const int64_t* prev_tokens;
-  const int* feed_prev;
-  const int* positions;
-  const int* slots;
-  const int* block_tables;
-  const int* seq_kvlen;
-  const float* cos_sin;
-  const float* temperature;
-  const int64_t* seeds;
-  const int64_t* steps;
-  void* x;
-  void* q;
-  void* attn;
-  void* act;
-  float* part_out;
-  float* part_lse;
-  int* att_counters;
-  unsigned long long* keys;
-  int64_t* tokens;
-  unsigned* sync;
-};
-int atta_decode_step(const DecodeStepArgs& a, hipStream_t stream);
-int64_t atta_decode_step_sync_words(int layers);
-int64_t atta_decode_step_error_index(int layers);
-int atta_decode_step_grid();
-// profiling buffers of later persistent-step launches (nullptr: off): see decode_step.hip
-void atta_set_decode_step_trace(void* trace, void* stats);
-
 // Prefill GEMM (prefill_gemm.hip): c[M, N] = a[M, K] . w[N, K]^T; mode 0 plain, 1 c = res +
 // a.w^T (res may alias c), 2 c = silu(a.gate^T) * (a.up^T) with w = [gate; up].  fp8: a / w are
 // e4m3fn bytes with fp32 row scales xs [M] / wsc [rows of w]; else bf16.  schedule -1 = the

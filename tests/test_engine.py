@@ -391,50 +391,6 @@ def test_long_context_decode(max_len):
     assert len(outs[0].token_ids) == 6
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("graphs", [False, True])
-def test_decode_megakernel_matches_oracle(graphs):
-    """The persistent decode step (ops/csrc/decode_step.hip: the whole decode forward in ONE
-    launch) on the Llama-3.1-8B layer geometry against the fp32 dense oracle (near-tie rule),
-    eager and graph-replayed; its bounded waits all succeeded (error word 0) and the fused
-    multi-kernel path would have been the alternative (it is what the flag replaces)."""
-    cfg = EngineConfig(model="llama-8b-slice", device="cuda", max_model_len=1024,
-                       num_kv_blocks=512, max_num_batched_tokens=256, max_num_seqs=8,
-                       use_graphs=graphs, graph_batch_sizes=(1, 2, 4, 8),
-                       decode_megakernel=True)
-    eng = LLMEngine(cfg)
-    r = eng.runner
-    assert r.mk_sync is not None, "megakernel not enabled for the 8B geometry"
-    prompts = _prompts(vocab=16000)
-    # a context past several 128-token partitions (multi-partition split-K combine)
-    prompts.append(list(np.random.default_rng(9).integers(300, 16000, size=700)))
-    outs, bad = _check(eng, prompts, n=8, tol_logit=0.25)
-    assert bad <= 2
-    from agentic_traffic_testing_amd import ops
-    assert ops.decode_step_error(r.mk_sync, r.mcfg.num_layers) == 0
-    if graphs:
-        assert r.graph_steps > 0
-
-
-@pytest.mark.gpu
-def test_decode_megakernel_sampling_replays():
-    """Seeded sampled decoding through the persistent step: graph replay == eager, token for
-    token (both run the same kernel; only launch mode differs)."""
-    res = []
-    for graphs in (False, True):
-        cfg = EngineConfig(model="llama-8b-slice", device="cuda", max_model_len=1024,
-                           num_kv_blocks=512, max_num_seqs=8, use_graphs=graphs,
-                           graph_batch_sizes=(1, 2, 4, 8), decode_megakernel=True)
-        eng = LLMEngine(cfg)
-        sp = [SamplingParams(temperature=0.7, max_tokens=12, ignore_eos=True, seed=100 + i)
-              for i in range(5)]
-        outs = eng.generate(_prompts(vocab=16000), sp)
-        res.append([o.token_ids for o in outs])
-        del eng
-        torch.cuda.empty_cache()
-    assert res[0] == res[1]
-
-
 def _check_fp8(eng, prompts, n, tol_logit):
     """Teacher-forced check of EVERY generated position: the oracle runs on the engine's own
     prefix (prompt + the engine's tokens so far), so one near-tie flip does not hide later
