@@ -218,6 +218,13 @@ class EngineConfig:
     # the measured A/B at that size: models/llama.py LlamaModel._PG_AUTO)
     prefill_gemm: str = "auto"
     prefill_gemm_min_rows: int = 128
+    # library prefill GEMMs from a TunableOp solution table (rocBLAS / hipBLASLt solution per
+    # exact shape, tuned cold on MI355X by scripts/gpu/tune_prefill_gemms.py): "auto" = the
+    # table shipped for this GPU (agentic_traffic_testing_amd/tuning/), "" = off, else a path.
+    # With a table, prefill steps pad their row count to the table's buckets
+    # (tuning.bucket_rows) - padding rows carry slot -1 and are never written to the KV cache
+    # or sampled
+    gemm_tuning: str = "auto"
     # async look-ahead decode: launch the next decode graph step before waiting for the
     # current one's tokens (llm_engine.LLMEngine.step)
     async_decode: bool = True

@@ -119,6 +119,13 @@ class ModelRunner:
                                 quantization=cfg.quantization)
         self.model.prefill_gemm = cfg.prefill_gemm
         self.model.prefill_gemm_min_rows = cfg.prefill_gemm_min_rows
+        # tuned library-GEMM table (agentic_traffic_testing_amd/tuning): prefill steps pad
+        # their rows to its buckets so their GEMMs hit tuned shapes
+        self.gemm_table = None
+        if self.device.type == "cuda" and cfg.gemm_tuning:
+            from .. import tuning
+
+            self.gemm_table = tuning.load(cfg.gemm_tuning, model_cfg.name)
         if weights_dir and cfg.load_format != "dummy":
             self.model.load_safetensors(weights_dir)
         else:
@@ -155,6 +162,10 @@ class ModelRunner:
         self.graph_sizes = [b for b in self.graph_sizes if b <= cap]
         self.max_seqs = max(cfg.max_num_seqs, self.graph_sizes[-1] if self.graph_sizes else 1)
         self.max_tokens = cfg.max_num_batched_tokens + self.max_seqs
+        if self.is_cuda and cfg.gemm_tuning:  # room for prefill row padding (tuning buckets)
+            from ..tuning import bucket_rows
+
+            self.max_tokens = bucket_rows(self.max_tokens)
         self._alloc_kv()
         self.bm = BlockManager(self.num_blocks, self.block_size, cfg.enable_prefix_caching)
         # metadata buffers (max layout)
@@ -284,8 +295,14 @@ class ModelRunner:
 
     def _prepare(self, batch: Batch, pad_seqs: int = 0, tiles: bool = True):
         ids, qs, ql = batch.arrays()
+        pad_tokens = 0
+        if tiles and self.gemm_table is not None and batch.num_decode < len(batch.seqs):
+            from ..tuning import bucket_rows
+
+            pad_tokens = bucket_rows(int(np.sum(ql)))
         d = self.bm.build_batch(ids, qs, ql, self.bt_width,
-                                self.tile_tokens if tiles else 0, batch.num_decode, 0, pad_seqs)
+                                self.tile_tokens if tiles else 0, batch.num_decode, pad_tokens,
+                                pad_seqs)
         T = d["positions"].shape[0]
         S = d["seq_kvlen"].shape[0]
         NT = d["tile_seq"].shape[0]
