@@ -241,6 +241,9 @@ class EngineConfig:
     tp_backend: str = "auto"
     tp_same_device: bool = False
     tp_allreduce: str = "auto"           # auto | rccl | ipc (custom one-shot all-reduce)
+    # IPC path: the row-parallel o / down decode GEMVs push their partial products straight
+    # into the peers' receive slots (all-reduce push fused into the GEMV epilogue)
+    tp_fused_push: bool = True
     dist_port: int = 0                   # 0 = pick a free port
     # a TP worker that has not registered on the step channel this long after rank 0
     # created it is reported dead (covers workers that die while loading weights)

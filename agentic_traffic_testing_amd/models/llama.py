@@ -472,6 +472,12 @@ class LlamaModel:
                 ops.linear(a2, L.o_ps if ps else L.o, residual=residual,
                            waves=ops.decode_waves("o", ps, L.o_s is not None),
                            preshuffled=ps, w_scale=L.o_s, ksplit=None, proj="o")
+            elif self.tp_group.push_ok(B, L.o.shape[0]):
+                # X1: the GEMV epilogue pushes into the peers' slots; one receive kernel
+                # adds the rank-order sum into the residual (no standalone one-shot kernel)
+                ops.linear_push_reduce(a2, L.o_ps if ps else L.o, residual, self.tp_group.ipc,
+                                       waves=ops.decode_waves("o", ps, L.o_s is not None),
+                                       preshuffled=ps, w_scale=L.o_s, proj="o")
             else:
                 self.tp_group.all_reduce_residual(
                     ops.linear(a2, L.o_ps if ps else L.o, preshuffled=ps, w_scale=L.o_s,
@@ -483,6 +489,11 @@ class LlamaModel:
                            waves=ops.decode_waves("down", ps, L.down_s is not None),
                            preshuffled=ps, w_scale=L.down_s, ksplit=None,
                            proj="down")
+            elif self.tp_group.push_ok(B, L.down.shape[0]):
+                ops.linear_push_reduce(act, L.down_ps if ps else L.down, residual,
+                                       self.tp_group.ipc,
+                                       waves=ops.decode_waves("down", ps, L.down_s is not None),
+                                       preshuffled=ps, w_scale=L.down_s, proj="down")
             else:
                 self.tp_group.all_reduce_residual(
                     ops.linear(act, L.down_ps if ps else L.down, preshuffled=ps,

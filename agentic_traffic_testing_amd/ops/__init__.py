@@ -635,6 +635,23 @@ def linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = Non
     return y
 
 
+def linear_push_reduce(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, ipc,
+                       waves: int | None = None, preshuffled: bool = False,
+                       w_scale: torch.Tensor | None = None, proj: str = "") -> torch.Tensor:
+    """TP row-parallel projection with the all-reduce push fused into the decode GEMV
+    (SURVEY §2.5 X1 / X2): the GEMV epilogue writes this rank's partial product into every
+    rank's IPC receive slot, then one receive kernel adds the rank-order sum into
+    ``residual`` (returned).  ``ipc``: the TP group's IpcAllReduce."""
+    if w_scale is not None:
+        preshuffled = True
+    if not skinny_ok(x, w):
+        raise ValueError("linear_push_reduce: decode-sized rows only")
+    n_out = w.shape[0]
+    ksplit = _ksplit(proj, x, None, n_out // 16)
+    ipc.gemv_push(x, w, n_out, waves or SKINNY_WAVES, preshuffled, w_scale, ksplit)
+    return ipc.push_reduce(residual, n_out)
+
+
 # ---- fused decode-step ops (norm weight folded into W on the host) -----------------------
 def decode_qkv_rope(x, w, eps, positions, slots, cos_sin, k_cache, v_cache, n_q_heads,
                     n_kv_heads, q_out=None, preshuffled=False, w_scale=None, ksplit=None):

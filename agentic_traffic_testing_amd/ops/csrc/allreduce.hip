@@ -338,6 +338,102 @@ static int launch(const Params& p, const void* x, void* y, const void* res, int6
 }
 
 
+// ---- X1 / X2 with the push fused into the row-parallel GEMV (ar_push_reduce) ------------
+// The one-shot kernel above reads the GEMV's output back from HBM, pushes it to the peers,
+// fences and flags - a launch of its own between the GEMV and the next layer step.  With the
+// push fused, the row-parallel o / down GEMV (skinny.h, EPI_PLAIN with SkinnyParams::push_*)
+// writes every finished 16-column tile straight into slot (parity, my rank) of every peer's
+// buffer, fences, and bumps that peer's 64-bit per-source tile counter; what is left here is
+// the receive side: wait until every source's counter covers this call's tiles, then the
+// rank-order fp32 sum (+ the residual add) of the W slots.  Same buffers, same per-block
+// generation counters and parity as the one-shot kernel (the GEMV reads the generation from
+// counter 0), so both kernels can be mixed on one buffer; the tile counters are monotonic
+// (64-bit, never reset) and each block keeps the cumulative count it expects in the header.
+constexpr size_t kPushRegion = 48 * 1024;  // per-source tile counters + per-block expectations
+static_assert(kPushRegion > 8192 + 256 + 2 * kMaxRanks * 256 * 8, "push region overlaps keys");
+static_assert(kPushRegion + 1024 + kMaxBlocks * 8 <= kHeaderBytes, "push region");
+static_assert(arl::kPushOffset == kPushRegion && arl::kSlotOffset == kHeaderBytes &&
+                  arl::kGenOffset == kFlagBytes && arl::kMaxRanks == kMaxRanks,
+              "common.h arl layout");
+
+__device__ __forceinline__ unsigned long long* push_ctr(uint8_t* base, int src) {
+  return reinterpret_cast<unsigned long long*>(base + kPushRegion + src * 64);
+}
+__device__ __forceinline__ unsigned long long* push_exp(uint8_t* base, int blk) {
+  return reinterpret_cast<unsigned long long*>(base + kPushRegion + 1024) + blk;
+}
+
+template <typename T, int W>
+__global__ void __launch_bounds__(kThreads) push_reduce_kernel(Params p, uint16_t* y,
+                                                               const uint16_t* res, int64_t n,
+                                                               int ntiles) {
+  const int b = blockIdx.x;
+  const int nb = gridDim.x;
+  uint8_t* mine = p.base[p.rank];
+  uint32_t* counters = reinterpret_cast<uint32_t*>(mine + kFlagBytes);
+  __shared__ uint32_t gen_s;
+  __shared__ unsigned long long exp_s;
+  if (threadIdx.x == 0) {
+    gen_s = counters[b] + 1;
+    exp_s = *push_exp(mine, b) + static_cast<unsigned long long>(ntiles);
+  }
+  __syncthreads();
+  const uint32_t gen = gen_s;
+  const unsigned long long want = exp_s;
+  const int par = gen & 1;
+  if (threadIdx.x < W) {
+    const unsigned long long* c = push_ctr(mine, threadIdx.x);
+    uint32_t spins = 0;
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 25)) {  // bounded: a dead peer must not hang the GPU
+        atomicOr(counters + kMaxBlocks, 1u << threadIdx.x);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, once after the poll
+  }
+  __syncthreads();
+  int64_t per = (n + nb - 1) / nb;
+  per = (per + 7) & ~int64_t(7);
+  const int64_t beg = b * per < n ? b * per : n;
+  const int64_t end = beg + per < n ? beg + per : n;
+  using V = Pack8;
+  for (int64_t i = beg + 8 * threadIdx.x; i < end; i += 8 * kThreads) {
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    const int cnt = i + 8 <= end ? 8 : static_cast<int>(end - i);
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      const uint16_t* src = slot_ptr(mine, par, q, p.max_elems) + i;
+      if (cnt == 8) {
+        const V v = *reinterpret_cast<const V*>(src);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += to_f32<T>(v.v[j]);
+      } else {
+        for (int j = 0; j < cnt; ++j) acc[j] += to_f32<T>(src[j]);
+      }
+    }
+    if (res != nullptr) {
+      for (int j = 0; j < cnt; ++j) acc[j] = to_f32<T>(from_f32<T>(acc[j])) + to_f32<T>(res[i + j]);
+    }
+    if (cnt == 8) {
+      V o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o.v[j] = from_f32<T>(acc[j]);
+      *reinterpret_cast<V*>(y + i) = o;
+    } else {
+      for (int j = 0; j < cnt; ++j) y[i + j] = from_f32<T>(acc[j]);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    counters[b] = gen;
+    *push_exp(mine, b) = want;
+  }
+}
+
 // ---- X4: int64 MAX of the vocab-parallel sampler keys (one tiny block) ------------------
 // Each rank's LM-head shard reduces a decode row to one signed-orderable packed
 // (score, -token) key; the MAX over ranks is the global Gumbel-max winner.  Same push /
@@ -501,4 +597,44 @@ int atta_ar2_run(void* const* bases, int rank, int world, int64_t max_elems, con
   p.chunk_max = chunk_max_of(max_elems, world);
   return dtype == 0 ? ar::launch2<__bf16>(p, x, y, res, n, stream)
                     : ar::launch2<_Float16>(p, x, y, res, n, stream);
+}
+
+// Receive side of the GEMV-fused push (see push_reduce_kernel): y = sum over ranks of the
+// pushed slots (+ res), n elements; ntiles = tiles each source's GEMV pushed for this call.
+int atta_ar_push_reduce(void* const* bases, int rank, int world, int64_t max_elems, void* y,
+                        const void* res, int64_t n, int ntiles, int dtype, hipStream_t stream) {
+  if (world != 2 && world != 4 && world != 8) return -1;
+  if (rank < 0 || rank >= world || n <= 0 || n > max_elems || ntiles <= 0) return -1;
+  ar::Params p{};
+  for (int i = 0; i < world; ++i) p.base[i] = static_cast<uint8_t*>(bases[i]);
+  p.rank = rank;
+  p.world = world;
+  p.max_elems = max_elems;
+  uint16_t* yo = static_cast<uint16_t*>(y);
+  const uint16_t* ri = static_cast<const uint16_t*>(res);
+#define ATTA_PR(T_)                                                                            \
+  switch (world) {                                                                             \
+    case 2: ar::push_reduce_kernel<T_, 2><<<ar::kMaxBlocks, ar::kThreads, 0, stream>>>(p, yo, ri, n, ntiles); break; \
+    case 4: ar::push_reduce_kernel<T_, 4><<<ar::kMaxBlocks, ar::kThreads, 0, stream>>>(p, yo, ri, n, ntiles); break; \
+    default: ar::push_reduce_kernel<T_, 8><<<ar::kMaxBlocks, ar::kThreads, 0, stream>>>(p, yo, ri, n, ntiles); break; \
+  }
+  if (dtype == 0) {
+    ATTA_PR(__bf16)
+  } else {
+    ATTA_PR(_Float16)
+  }
+#undef ATTA_PR
+  return static_cast<int>(hipGetLastError());
+}
+
+// Layout constants the GEMV's push epilogue needs (skinny.h): byte offsets of the generation
+// counter 0, of the slots and of the per-source tile counters inside a rank's buffer.
+int64_t atta_ar_push_layout(int what) {
+  switch (what) {
+    case 0: return static_cast<int64_t>(ar::kFlagBytes);   // uint32 generation counter 0
+    case 1: return static_cast<int64_t>(ar::kHeaderBytes); // slot (par, src) base
+    case 2: return static_cast<int64_t>(ar::kPushRegion);  // uint64 counter of source q at +64 q
+    case 3: return ar::kMaxRanks;
+    default: return -1;
+  }
 }

@@ -631,6 +631,45 @@ void ar_run(const at::Tensor& x, at::Tensor y, at::IntArrayRef bases, int64_t ra
            "ar_run");
 }
 
+// Row-parallel TP GEMV with the all-reduce push fused (X1 / X2): x @ w^T of this rank's K
+// shard goes straight into every rank's IPC receive slot; ar_push_reduce finishes the sum.
+void skinny_gemm_push(const at::Tensor& x, const at::Tensor& w, int64_t n_out, int64_t waves,
+                      bool preshuffled, const c10::optional<at::Tensor>& w_scale, int64_t ksplit,
+                      at::IntArrayRef bases, int64_t rank, int64_t max_elems) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.is_contiguous(),
+              "skinny_gemm_push: layout");
+  TORCH_CHECK(x.size(1) == w.size(1) && w.size(0) == n_out &&
+                  (x.scalar_type() == w.scalar_type() || w.scalar_type() == at::kByte),
+              "skinny_gemm_push: shapes / dtypes");
+  TORCH_CHECK(bases.size() >= 2 && bases.size() <= 8, "skinny_gemm_push: 2..8 ranks");
+  const float* ws = fp8_scale(w, w_scale, "skinny_gemm_push");
+  void* b[8] = {};
+  for (size_t i = 0; i < bases.size(); ++i) b[i] = reinterpret_cast<void*>(bases[i]);
+  const at::DeviceGuard g(x.device());
+  check_rc(atta_skinny_gemm_push(x.data_ptr(), w.data_ptr(), x.size(0), w.size(0), w.size(1),
+                                 x.stride(0), waves, ksplit, ws, skinny_dtype(x, preshuffled),
+                                 b, static_cast<int>(rank), static_cast<int>(bases.size()),
+                                 max_elems, cur_stream()),
+           "skinny_gemm_push");
+}
+
+// Receive side: y (+)= sum over ranks of the pushed [rows, n] products (rank order, fp32);
+// with residual: y = residual + sum (y may alias residual).  ntiles = tiles each source pushed.
+void ar_push_reduce(at::Tensor y, const c10::optional<at::Tensor>& residual,
+                    at::IntArrayRef bases, int64_t rank, int64_t max_elems, int64_t ntiles) {
+  check_dev(y, "y");
+  TORCH_CHECK(y.is_contiguous(), "ar_push_reduce: layout");
+  TORCH_CHECK(bases.size() >= 2 && bases.size() <= 8, "ar_push_reduce: 2..8 ranks");
+  void* b[8] = {};
+  for (size_t i = 0; i < bases.size(); ++i) b[i] = reinterpret_cast<void*>(bases[i]);
+  const at::DeviceGuard g(y.device());
+  check_rc(atta_ar_push_reduce(b, static_cast<int>(rank), static_cast<int>(bases.size()),
+                               max_elems, y.data_ptr(), res_ptr(residual, y, "ar_push_reduce"),
+                               y.numel(), static_cast<int>(ntiles), dtype_code(y), cur_stream()),
+           "ar_push_reduce");
+}
+
 void ar_keymax(at::Tensor keys, const c10::optional<at::Tensor>& tokens, at::IntArrayRef bases,
                int64_t rank) {
   check_dev(keys, "keys");
@@ -726,6 +765,10 @@ std::vector<std::string> graph_nodes(int64_t graph) {
 TORCH_LIBRARY(atta, m) {
   m.def("graph_nodes(int graph) -> str[]", &graph_nodes);
   m.def("ar_buffer_bytes(int max_elems, int elem_bytes) -> int", &ar_buffer_bytes);
+  m.def("skinny_gemm_push(Tensor x, Tensor w, int n_out, int waves, bool preshuffled, "
+        "Tensor? w_scale, int ksplit, int[] bases, int rank, int max_elems) -> ()");
+  m.def("ar_push_reduce(Tensor(a!) y, Tensor? residual, int[] bases, int rank, int max_elems, "
+        "int ntiles) -> ()");
   m.def("ar_alloc(int bytes, int device) -> int", &ar_alloc);
   m.def("set_attention_trace(Tensor? trace) -> ()", &set_attention_trace);
   m.def("set_gemv_trace(Tensor? trace) -> ()", &set_gemv_trace);
@@ -797,6 +840,8 @@ TORCH_LIBRARY(atta, m) {
 
 TORCH_LIBRARY_IMPL(atta, CUDA, m) {
   m.impl("ar_run", &ar_run);
+  m.impl("skinny_gemm_push", &skinny_gemm_push);
+  m.impl("ar_push_reduce", &ar_push_reduce);
   m.impl("ar2_run", &ar2_run);
   m.impl("ar_keymax", &ar_keymax);
   m.impl("rms_norm", &rms_norm);

@@ -111,6 +111,14 @@ __device__ __forceinline__ float dev_load4(__amdgpu_buffer_rsrc_t r, uint32_t of
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, kScDevice));
 }
 
+// ---- IPC all-reduce buffer layout shared by allreduce.hip and the GEMV push epilogue ----
+namespace arl {
+constexpr int kMaxRanks = 8;
+constexpr size_t kGenOffset = 2 * kMaxRanks * 32 * sizeof(uint32_t);  // uint32 generation, block 0
+constexpr size_t kSlotOffset = 64 * 1024;                              // slots (parity, src)
+constexpr size_t kPushOffset = 48 * 1024;  // uint64 tile counter of source q at + 64 q
+}  // namespace arl
+
 // ---- wave / block reductions -----------------------------------------------------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

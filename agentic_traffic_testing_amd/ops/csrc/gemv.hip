@@ -269,6 +269,41 @@ int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual
   return static_cast<int>(hipGetLastError());
 }
 
+// Row-parallel TP GEMV with the all-reduce push fused into its epilogue: x W^T of this rank's
+// K shard goes straight into slot (parity, rank) of every rank's IPC buffer (bases[q]); the
+// receive side is atta_ar_push_reduce (allreduce.hip), which also adds the residual.
+int atta_skinny_gemm_push(const void* x, const void* w, int M, int N, int K, int64_t x_stride,
+                          int waves, int ksplit, const float* wscale, int dtype,
+                          void* const* bases, int rank, int world, int64_t max_elems,
+                          hipStream_t stream) {
+  const int ps = (dtype & kPreshuffled) ? 1 : 0;
+  dtype &= ~kPreshuffled;
+  if (M < 1 || M > 32 || N % 16 != 0) return -1;
+  if ((world != 2 && world != 4 && world != 8) || rank < 0 || rank >= world ||
+      static_cast<int64_t>(M) * N > max_elems)
+    return -1;
+  SkinnyParams p{};
+  p.ps = ps;
+  p.wscale = wscale;
+  p.x = static_cast<const uint16_t*>(x);
+  p.w = static_cast<const uint16_t*>(w);
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.x_stride = x_stride;
+  p.eps = 0.f;
+  for (int q = 0; q < world; ++q) p.push_base[q] = static_cast<uint8_t*>(bases[q]);
+  p.push_world = world;
+  p.push_rank = rank;
+  p.push_max_elems = max_elems;
+  if (const int rc = setup_split(p, waves, ksplit, N / 16, wscale != nullptr)) return rc;
+  const int mt = M <= 16 ? 1 : 2;
+  dim3 grid(N / 16, p.ksplit);
+  p.wg_trace = take_trace();
+  launch_epi<EPI_PLAIN>(dtype, mt, waves, grid, stream, p);
+  return static_cast<int>(hipGetLastError());
+}
+
 int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x, const void* w,
                         const int* positions, const int* slots, const float* cos_sin, int M,
                         int K, int64_t x_stride, int64_t q_stride, int n_q_heads, int n_kv_heads,

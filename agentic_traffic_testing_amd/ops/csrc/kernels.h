@@ -59,6 +59,13 @@ int atta_sample_topkp(int64_t* out, const void* logits, int rows, int vocab, int
                       const int* top_k, const int64_t* seeds, const int64_t* steps,
                       hipStream_t stream);
 
+int atta_skinny_gemm_push(const void* x, const void* w, int M, int N, int K, int64_t x_stride,
+                          int waves, int ksplit, const float* wscale, int dtype,
+                          void* const* bases, int rank, int world, int64_t max_elems,
+                          hipStream_t stream);
+int atta_ar_push_reduce(void* const* bases, int rank, int world, int64_t max_elems, void* y,
+                        const void* res, int64_t n, int ntiles, int dtype, hipStream_t stream);
+int64_t atta_ar_push_layout(int what);
 int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual, int M, int N,
                      int K, int64_t x_stride, int64_t y_stride, int64_t res_stride, int waves,
                      int ksplit, const float* wscale, int dtype, hipStream_t stream);

@@ -94,6 +94,13 @@ struct SkinnyParams {
   // optional per-workgroup timeline (ops.set_gemv_trace): [start, end] on the 100 MHz wall
   // clock per workgroup of the grid (gridDim.y == 1 launches only)
   unsigned long long* wg_trace;
+  // TP row-parallel GEMV with the all-reduce push fused (allreduce.hip push_reduce_kernel):
+  // push_world > 0 turns the PLAIN epilogue into "write this tile into slot (parity,
+  // push_rank) of every rank's IPC buffer, fence, bump that rank's tile counter for this
+  // source" - the [M, N] product never lands in local memory
+  uint8_t* push_base[arl::kMaxRanks];
+  int push_world, push_rank;
+  int64_t push_max_elems;
 };
 
 __device__ __forceinline__ unsigned ordered_bits(float f) {
@@ -324,6 +331,34 @@ __device__ __forceinline__ void skinny_body(const SkinnyParams& p, const int til
   __syncthreads();
 
   // ---- epilogues -----------------------------------------------------------------------
+  if constexpr (EPI == EPI_PLAIN) {
+    if (p.push_world > 0) {
+      // generation of this call = the receive kernel's last completed generation + 1 (read
+      // from this rank's own buffer; stream order makes the previous call's value final)
+      const uint32_t gen = __hip_atomic_load(reinterpret_cast<const uint32_t*>(
+                                                 p.push_base[p.push_rank] + arl::kGenOffset),
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
+      const int par = gen & 1;
+      for (int e = threadIdx.x; e < R * 16; e += WAVES * 64) {
+        const int m = e >> 4, n = e & 15;
+        if (m >= p.M) continue;
+        float v = red[0][m][n];
+        if (norm) v *= inv_rms[m];
+        const uint16_t o = from_f32<T>(v);
+        const int64_t off = (static_cast<int64_t>(par) * arl::kMaxRanks + p.push_rank) *
+                                p.push_max_elems + static_cast<int64_t>(m) * p.N + tile * 16 + n;
+        for (int q = 0; q < p.push_world; ++q)
+          reinterpret_cast<uint16_t*>(p.push_base[q] + arl::kSlotOffset)[off] = o;
+      }
+      __threadfence_system();  // this tile's stores reach every peer before its counter bump
+      __syncthreads();
+      if (threadIdx.x < p.push_world)
+        __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(
+                                   p.push_base[threadIdx.x] + arl::kPushOffset + 64 * p.push_rank),
+                               1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+  }
   if constexpr (EPI == EPI_PLAIN || EPI == EPI_RESADD) {
     for (int e = threadIdx.x; e < R * 16; e += WAVES * 64) {
       const int m = e >> 4, n = e & 15;

@@ -60,6 +60,14 @@ class TPComm:
             return self.ipc.all_reduce(x, residual=residual)
         return residual.add_(self.all_reduce(x))
 
+    def push_ok(self, rows: int, n_out: int) -> bool:
+        """Can a row-parallel decode GEMV push its product straight into the peers'
+        receive slots (IPC path, fused push)?"""
+        return (self.size > 1 and self.ipc is not None and self.fused_push
+                and self.ipc.push_eligible(rows, n_out))
+
+    fused_push: bool = True
+
     @property
     def decode_capturable(self) -> bool:
         """Can a decode step's collectives (X1/X2 sums, X4 key MAX) be hipGraph-captured?

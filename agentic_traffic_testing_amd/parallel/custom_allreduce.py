@@ -91,6 +91,7 @@ class IpcAllReduce:
         self.calls = 0
         self.calls2 = 0
         self.calls_max = 0
+        self.calls_push = 0
 
     def _ok(self, x: torch.Tensor) -> bool:
         return (x.is_cuda and x.is_contiguous() and x.dtype in (torch.bfloat16, torch.float16)
@@ -119,6 +120,26 @@ class IpcAllReduce:
             self._ops.ar_run(x, y, self.bases, self.comm.rank, self.max_elems, residual)
             self.calls += 1
         return y
+
+    # -- X1 / X2 with the push fused into the row-parallel GEMV ------------------------------
+    def push_eligible(self, rows: int, n_out: int) -> bool:
+        return rows * n_out <= self.max_elems and n_out % 16 == 0
+
+    def gemv_push(self, x: torch.Tensor, w: torch.Tensor, n_out: int, waves: int,
+                  preshuffled: bool, w_scale, ksplit: int) -> None:
+        """Row-parallel decode GEMV whose epilogue writes x @ w.T of this rank's K shard
+        straight into every rank's receive slot (no local output, no separate push);
+        ``push_reduce`` completes the all-reduce."""
+        self._ops.skinny_gemm_push(x, w, n_out, waves, preshuffled, w_scale, ksplit,
+                                   self.bases, self.comm.rank, self.max_elems)
+
+    def push_reduce(self, residual: torch.Tensor, n_out: int) -> torch.Tensor:
+        """residual += sum over ranks of the pushed products (rank-order fp32 sum, the
+        residual add in the same kernel); n_out / 16 tiles were pushed by every source."""
+        self._ops.ar_push_reduce(residual, residual, self.bases, self.comm.rank,
+                                 self.max_elems, n_out // 16)
+        self.calls_push += 1
+        return residual
 
     MAX_KEYS = 256
 

@@ -110,6 +110,7 @@ def _maybe_ipc(cfg: EngineConfig, comm, runner: ModelRunner):
     H = runner.mcfg.hidden_size
     comm.ipc = IpcAllReduce(comm, runner.device, max_bytes=runner.max_seqs * H * 2,
                             large_max_bytes=min(cfg.max_num_batched_tokens, 8192) * H * 2)
+    comm.fused_push = bool(getattr(cfg, "tp_fused_push", True))
 
 
 class TPEngine(LLMEngine):

@@ -255,15 +255,18 @@ def test_tp2_same_gpu_rehearsal_host_collectives():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tp,model", [(2, "small"), (4, "llama-70b-tp-slice"),
-                                      (8, "llama-70b-tp-slice")])
-def test_tp_same_gpu_graph_captured_decode(tp, model):
+@pytest.mark.parametrize("tp,model,push", [(2, "small", True), (4, "llama-70b-tp-slice", True),
+                                           (8, "llama-70b-tp-slice", True),
+                                           (8, "llama-70b-tp-slice", False)])
+def test_tp_same_gpu_graph_captured_decode(tp, model, push):
     """TP=2/4/8 on ONE MI355X with hipGraph-captured decode.  Every decode-step
     collective is an IPC kernel on the peer buffers (X1/X2 sums with the residual add fused
     into the epilogue, X4 sampler-key MAX writing the token ids), so the whole step - every
     rank's 5 kernels x layers + 2 all-reduces per layer + LM head + key MAX - is captured and
     replayed although the control group is gloo.  Greedy tokens equal TP=1's (graphs on) up to
-    a late bf16 near-tie flip; the IPC timeout word stays 0."""
+    a late bf16 near-tie flip; the IPC timeout word stays 0.  push=True (the default): the o /
+    down GEMVs push their partials straight into the peers' slots (fused push) and one receive
+    kernel per projection adds the sum into the residual; push=False: GEMV + one-shot kernel."""
     base = dict(model=model, device="cuda:0", max_model_len=512, num_kv_blocks=128,
                 max_num_batched_tokens=256, max_num_seqs=4, use_graphs=True)
     greedy = SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True)
@@ -273,7 +276,7 @@ def test_tp_same_gpu_graph_captured_decode(tp, model):
     del ref_eng
     torch.cuda.empty_cache()
     eng = TPEngine(EngineConfig(tensor_parallel_size=tp, tp_same_device=True,
-                                tp_allreduce="ipc", **base))
+                                tp_allreduce="ipc", tp_fused_push=push, **base))
     try:
         r = eng.runner
         assert eng.comm.decode_capturable and r.graphs, "no decode graph was captured"
@@ -285,7 +288,8 @@ def test_tp_same_gpu_graph_captured_decode(tp, model):
         s2 = [o.token_ids for o in eng.generate(_prompts(), sampled)]
         assert s1 == s2  # seeded Gumbel draws: replay-deterministic across the TP group
         ipc = eng.comm.ipc
-        assert ipc.calls > 0 and ipc.calls_max > 0
+        assert ipc.calls_max > 0
+        assert (ipc.calls_push > 0) if push else (ipc.calls > 0 and ipc.calls_push == 0)
         assert ipc.check() == 0
     finally:
         eng.shutdown()
@@ -356,6 +360,87 @@ def _ipc_ar_worker(rank, world, port, q):
     except Exception as e:  # pragma: no cover
         import traceback
         q.put((rank, repr(e) + traceback.format_exc(), -1))
+
+
+def _ipc_push_worker(rank, world, port, q):
+    try:
+        from agentic_traffic_testing_amd import ops
+        from agentic_traffic_testing_amd.parallel.comm import init_distributed
+        from agentic_traffic_testing_amd.parallel.custom_allreduce import IpcAllReduce
+
+        torch.cuda.set_device(0)
+        comm = init_distributed(rank, world, "cuda:0", "gloo", "127.0.0.1", port)
+        ar = IpcAllReduce(comm, "cuda:0", max_bytes=16 * 8192 * 2)
+        bad = []
+        for it, (B, N, K) in enumerate([(1, 4096, 1024), (5, 8192, 1024), (16, 4096, 512),
+                                        (3, 4096, 3584)] * 3):
+            g = torch.Generator(device="cpu").manual_seed(100 * it + rank)
+            x = torch.randn(B, K, generator=g).to(torch.bfloat16).cuda()
+            w = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).cuda()
+            gr = torch.Generator(device="cpu").manual_seed(7 + it)  # same residual everywhere
+            res = torch.randn(B, N, generator=gr).to(torch.bfloat16).cuda()
+            # reference: the unfused path (GEMV, then the one-shot kernel with the residual add)
+            r1 = res.clone()
+            ar.all_reduce(ops.linear(x, w), residual=r1)
+            # fused push: the GEMV epilogue pushes, one receive kernel adds the sum
+            r2 = res.clone()
+            ops.linear_push_reduce(x, w, r2, ar)
+            torch.cuda.synchronize()
+            if not torch.equal(r1, r2):
+                bad.append((it, B, N, K, float((r1.float() - r2.float()).abs().max())))
+        # graph-captured replays of the push path with fresh inputs each time
+        B, N, K = 4, 4096, 1024
+        x = torch.empty(B, K, dtype=torch.bfloat16, device="cuda")
+        w = (torch.randn(N, K, device="cuda") / 32).to(torch.bfloat16)
+        r = torch.empty(B, N, dtype=torch.bfloat16, device="cuda")
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            ops.linear_push_reduce(x.fill_(0.5), w, r.fill_(0.0), ar)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            ops.linear_push_reduce(x, w, r, ar)
+        for k in range(4):
+            x.copy_(torch.full((B, K), 0.25 * (rank + k + 1), device="cuda").to(torch.bfloat16))
+            r.fill_(1.0)
+            graph.replay()
+            torch.cuda.synchronize()
+            exp = r.clone().fill_(1.0)
+            ar.all_reduce(ops.linear(x, w), residual=exp)
+            torch.cuda.synchronize()
+            if not torch.equal(r, exp):
+                bad.append(("graph", k))
+        if ar.check() != 0:
+            bad.append(("timeout-word", ar.check()))
+        comm.barrier()
+        ar.close()
+        q.put((rank, bad, ar.calls_push))
+        torch.distributed.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), -1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_ipc_fused_push_matches_oneshot(world):
+    """X1 / X2 with the push fused into the row-parallel GEMV (skinny.h push epilogue +
+    allreduce.hip push_reduce_kernel) is bit-identical to GEMV + one-shot kernel at 2 / 4 / 8
+    ranks on one MI355X, eager and graph-replayed, mixed with one-shot calls on one buffer."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_ipc_push_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    for rank, bad, calls in res:
+        assert bad == [], bad
+        assert calls > 10
 
 
 @pytest.mark.gpu
