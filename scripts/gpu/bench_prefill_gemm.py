@@ -58,8 +58,15 @@ def main():
                     help="schedules to sweep per call (default: --schedule)")
     ap.add_argument("--rounds", type=int, default=3,
                     help="interleaved rounds of all variants; the median is reported")
+    ap.add_argument("--tuned", default="",
+                    help="TunableOp table for the hipBLASLt arm (agentic_traffic_testing_amd/"
+                         "tuning; 'auto' = the shipped llama-3.1-8b table)")
     args = ap.parse_args()
     scheds = args.schedules or [args.schedule]
+    if args.tuned:
+        from agentic_traffic_testing_amd import tuning
+
+        print(f"# library arm on the tuned table: {tuning.load(args.tuned, 'llama-3.1-8b')}")
     ops.prefill_gemm_config(args.schedule, args.group_m)
     dev = "cuda"
     print(f"# prefill GEMM A/B ({'fp8 e4m3fn, row scales' if args.fp8 else 'bf16'}), "

@@ -6,7 +6,7 @@
 #   STAGES="bench prefill" bash scripts/gpu/stages.sh
 #
 # Stages:
-#   tests      pytest -m gpu (PYTEST_ARGS narrows it)
+#   tests      pytest -m gpu (PYTEST_ARGS: files; PYTEST_K: a -k expression)
 #   smoke      __graft_entry__.smoke()
 #   bench      bench.py --steps $STEPS --warmup 1 --verbose ($BENCH_ARGS)
 #   http       bench.py --via http ($BENCH_ARGS)
@@ -33,7 +33,7 @@ run() {  # name, timeout, cmd...
 for s in ${STAGES:-bench}; do
   case $s in
     tests) TAILN=6 run tests "${TEST_TIMEOUT:-900}" python -u -m pytest -x -q --timeout 240 \
-             --timeout-method thread -m gpu ${PYTEST_ARGS:-tests} ;;
+             --timeout-method thread -m gpu ${PYTEST_K:+-k "$PYTEST_K"} ${PYTEST_ARGS:-tests} ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py --steps "${STEPS:-2}" --warmup 1 --verbose ${BENCH_ARGS:-} ;;
     http) run http 900 python bench.py --via http --steps "${STEPS:-2}" --warmup 1 --verbose ${BENCH_ARGS:-} ;;
