@@ -46,13 +46,14 @@ def summarise(path: Path) -> str:
     lines = [f"== {path.name}: node kinds {dict(kinds)}"]
     for k, c in kern.most_common():
         tag = ""
-        if "oneshot_kernel" in k or "twoshot_kernel" in k or "keymax_kernel" in k:
+        if ("oneshot_kernel" in k or "twoshot_kernel" in k or "keymax_kernel" in k
+                or "push_reduce_kernel" in k):
             tag = "   <- IPC collective"
         elif re.search(r"nccl|rccl", k, re.I):
             tag = "   <- RCCL"
         lines.append(f"  {c:5d}  {k}{tag}")
     rccl = sum(c for k, c in kern.items() if re.search(r"nccl|rccl", k, re.I))
-    ipc = sum(c for k, c in kern.items() if re.search(r"oneshot|twoshot|keymax", k))
+    ipc = sum(c for k, c in kern.items() if re.search(r"oneshot|twoshot|keymax|push_reduce", k))
     lines.append(f"  -> IPC collective kernels {ipc}, RCCL kernels {rccl}, host nodes "
                  f"{kinds.get('host', 0)}")
     return "\n".join(lines)
