@@ -126,6 +126,7 @@ class ModelRunner:
             from .. import tuning
 
             self.gemm_table = tuning.load(cfg.gemm_tuning, model_cfg.name)
+        self.model.gemm_tuned = self.gemm_table is not None
         if weights_dir and cfg.load_format != "dummy":
             self.model.load_safetensors(weights_dir)
         else:
@@ -156,7 +157,7 @@ class ModelRunner:
         self.parts_buckets_small = sorted(
             {p for p in cfg.graph_parts_buckets if p < self.max_parts_small}
             | {self.max_parts_small})
-        self.tile_tokens = ops.prefill_tile_tokens(self.model.g)
+        self.tile_tokens = ops.prefill_tile_tokens(self.model.g, bt_width=self.bt_width)
         self.graph_sizes = sorted(b for b in cfg.graph_batch_sizes)
         cap = next((b for b in self.graph_sizes if b >= cfg.max_num_seqs), cfg.max_num_seqs)
         self.graph_sizes = [b for b in self.graph_sizes if b <= cap]

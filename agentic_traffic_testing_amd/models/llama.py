@@ -368,11 +368,16 @@ class LlamaModel:
         return ops.rms_norm(residual, self.norm, eps)
 
     # "auto" routing of the prefill projections: (weight dtype, mode) -> the smallest row count
-    # from which the hand-written GEMM beat hipBLASLt in the cold-weight A/B on the 8B shapes
-    # (profiles/r3_prefill_gemm_ab_*: fp8 gate_up+SiLU 1.03-1.19x from M 512, fp8 down 1.10-1.13x
-    # at M 2600, bf16 gate_up+SiLU 1.06-1.10x at M 2600; everything else stays on hipBLASLt)
-    _PG_AUTO = {(torch.uint8, "gate_up"): 512, (torch.uint8, "down"): 2048,
-                (torch.bfloat16, "gate_up"): 2048}
+    # from which the hand-written GEMM beat hipBLASLt in the cold-weight A/B on the 8B shapes.
+    # Round 4 re-measured against the library as the engine now runs it
+    # (profiles/r4_prefill_gemm_largem_ab.txt): bf16 on the tuned table (gemm_tuning) wins every
+    # projection at 2048-4096 rows (the hand-written gate_up+SiLU 0.84-0.88x), so bf16 routes
+    # here only when no tuned table is loaded (round 3: 1.06-1.10x over the untuned heuristic at
+    # 2600); fp8 gate_up+SiLU 1.08x at 3200, parity at 2048, 0.82-0.92x below; fp8 down
+    # 0.89-0.93x (was routed from 2048 in round 3).
+    _PG_AUTO = {(torch.uint8, "gate_up"): 2560}
+    _PG_AUTO_UNTUNED = {(torch.bfloat16, "gate_up"): 2048}
+    gemm_tuned = False  # set by the model runner when a tuned library table is loaded
     # row ranges where the split-K schedule (co-resident K slices of the few 256 x 256 tiles,
     # parallel reduction) beat hipBLASLt: bf16 down+residual 1.12-1.15x at M 512 / 1024, parity
     # at 400 (profiles/r3_prefill_gemm_ab_bf16_splitk.txt)
@@ -394,6 +399,8 @@ class LlamaModel:
         w = ops_[-1]
         if self.prefill_gemm == "auto":
             m = self._PG_AUTO.get((w.dtype, proj))
+            if m is None and not self.gemm_tuned:
+                m = self._PG_AUTO_UNTUNED.get((w.dtype, proj))
             if m is None or T < m:
                 return False
         elif self.prefill_gemm != "atta" or T < self.prefill_gemm_min_rows:

@@ -219,10 +219,19 @@ def rope_cache(qkv, positions, slot_mapping, cos_sin, k_cache, v_cache, n_q_head
 # (flash_prefill.hip, tiles of 128 / G tokens); "v1" = the round-1 per-wave kernel
 # (attention.hip, tiles of 64 / G ... 8 tokens; kept for A/B runs).
 PREFILL_IMPL = os.environ.get("ATTA_PREFILL_IMPL", "flash")
+# the flash kernel stages a sequence's whole block-table row in LDS (kBtLds entries: 32k
+# tokens at block size 16); wider tables take the v1 kernel
+FLASH_MAX_BT = 2048
 
 
-def prefill_tile_tokens(g: int, impl: str | None = None) -> int:
+def prefill_impl(bt_width: int = 0, impl: str | None = None) -> str:
+    impl = impl or PREFILL_IMPL
+    return "v1" if impl == "flash" and bt_width > FLASH_MAX_BT else impl
+
+
+def prefill_tile_tokens(g: int, impl: str | None = None, bt_width: int = 0) -> int:
     """Query tokens per prefill attention workgroup for GQA group ``g``."""
+    impl = prefill_impl(bt_width, impl)
     # 4 waves x (32 // g) tokens (flash: 32 columns per wave) or x (16 // g) (v1: 16) - the
     # G heads of a token share a wave; G = 3 (Llama-3.2-3B) leaves 2 resp. 1 columns idle
     if (impl or PREFILL_IMPL) == "flash":
@@ -239,7 +248,7 @@ def attention_prefill(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, 
         return ref.paged_attention(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart,
                                    scale, out=out)
     out = torch.empty_like(q) if out is None else out
-    fn = _native().flash_prefill if (impl or PREFILL_IMPL) == "flash" else \
+    fn = _native().flash_prefill if prefill_impl(block_tables.shape[1], impl) == "flash" else \
         _native().attention_prefill
     fn(out, q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, tile_seq, tile_qoff,
        q.shape[1], k_cache.shape[1], scale)

@@ -149,10 +149,10 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
   // thread t handles chunks t + 256 u
   constexpr int kChunks = kKB * 16 / 256;   // per thread, per tensor
   constexpr int kVq = kKB / 8;              // 8-key groups per V^T row
-  auto page_of = [&](int key) -> int {
-    const int i = key >> p.bs_shift;
-    return i < kBtLds ? lds_bt[i] : bt[i];
-  };
+  // LDS only (the launcher rejects bt_stride > kBtLds): a select between the LDS copy and the
+  // global table compiled to FLAT loads, whose vmcnt wait put a dependent global round trip
+  // in front of every block's K/V loads
+  auto page_of = [&](int key) -> int { return lds_bt[key >> p.bs_shift]; };
   const int64_t head_elems = static_cast<int64_t>(BS) * kD;  // per (page, head)
   u32x4 kr[kChunks], vr[kChunks];
   auto load_block = [&](int kb) {
@@ -208,8 +208,8 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
   for (int kb = 0; kb < nblocks; ++kb) {
     const int buf = kb & 1;
     const bool more = kb + 1 < nblocks;
-    if (more) load_block(kb + 1);  // in flight during this block's MFMAs
     const int k0 = kb * kKB;
+    bool issued = false;
     if (k0 < w_end) {  // wave-uniform: the wave has visible keys in this block
       const uint16_t* kl = lds_k[buf];
       const uint16_t* vl = lds_v[buf];
@@ -226,6 +226,12 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
           sacc[t] = MF::mma(kf, qf[st], sacc[t]);
         }
       }
+      // next block's K/V -> registers, issued after QK^T (guide §5.5 T14): in flight during
+      // softmax + PV.  Issued at the top of the loop instead, the first QK^T MFMA (whose
+      // accumulator the compiler had overlapped with the loads' address registers) waited
+      // vmcnt(0) for them: every block paid the whole load latency.
+      if (more) load_block(kb + 1);
+      issued = true;
       // mask (only blocks crossing the diagonal of the wave's first token, or kvlen)
       const bool need_mask = k0 + kKB > ctx0 + w_first + 1;
       float tmax = kNegInf;
@@ -290,6 +296,7 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
         }
       }
     }
+    if (more && !issued) load_block(kb + 1);  // waves with no visible key in this block
     if (more) store_block(buf ^ 1);
     __syncthreads();
   }
@@ -341,6 +348,7 @@ int atta_flash_prefill(void* out, const void* q, const void* k_cache, const void
   if (n_q_heads % n_kv_heads || G > 8 || ((G & (G - 1)) && G != 3)) return -1;
   // 16-byte row loads of q / stores of out need 8-element aligned row strides
   if (q_stride % 8 || out_stride % 4) return -1;
+  if (bt_stride > fp::kBtLds) return -1;  // the block-table row is staged whole in LDS
   if (num_tiles == 0) return 0;
   fp::FlashParams prm{};
   prm.out = static_cast<uint16_t*>(out);
