@@ -31,15 +31,26 @@ def timeit(fn, iters=20, reps=3):
 
 
 def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--impls", nargs="+", default=["flash", "v1"])
+    ap.add_argument("--hq", type=int, nargs="+", default=[32, 64])
+    ap.add_argument("--n", type=int, nargs="+", default=[0],
+                    help="causal sequence lengths (0 = the default shape list)")
+    a = ap.parse_args()
+    shapes = ((512, 512), (2600, 2600), (4096, 4096), (3000 + 700, 700), (8192, 8192))
+    if a.n != [0]:
+        shapes = tuple((n, n) for n in a.n)
     dt = torch.bfloat16
     print("== prefill attention (us / TFLOP/s)")
-    for hq, hkv in ((32, 8), (64, 8)):
-        for kv, ql in ((512, 512), (2600, 2600), (4096, 4096), (3000 + 700, 700), (8192, 8192)):
+    for hq, hkv in ((h, 8) for h in a.hq):
+        for kv, ql in shapes:
             k, v, bt, kvlen, qstart, T = _make_paged([(kv, ql)], hkv, 16, dt)
             q = torch.randn(T, hq, 128, dtype=dt, device="cuda")
             flops = 4 * 128 * hq * (ql * (kv - ql) + ql * (ql + 1) / 2)
             row = f"Hq={hq:2d} kv={kv:5d} q={ql:5d} |"
-            for impl in ("flash", "v1"):
+            for impl in a.impls:
                 ts, to = _tiles([(kv, ql)], ops.prefill_tile_tokens(hq // hkv, impl))
                 out = torch.empty_like(q)
                 t = timeit(lambda: ops.attention_prefill(q, k, v, bt, kvlen, qstart, ts, to,
