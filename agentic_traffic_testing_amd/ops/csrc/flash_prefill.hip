@@ -18,8 +18,9 @@
 //   O^T[128 x 32] += V^T[128 x 32 keys] . P^T[32 keys x 32]    8 x mfma_f32_32x32x16
 //     B = P^T straight from the S^T accumulator registers (pairs packed to 16 bit; the k order
 //     inside a step is permuted, and the V^T A-operand reads follow the same permutation),
-//     A = V^T rows from LDS (two 8 B reads per fragment; rows padded to 72 B: conflict-free).
-// 64-key blocks (two 32-key sub-tiles).  O^T is rescaled only when a running max moved.
+//     A = V^T rows from LDS (one 16 B read per fragment from a key-permuted, padded image).
+// 64-key blocks (two 32-key sub-tiles).  O^T is rescaled only when a running max grew by more
+// than 2^8 (defer-max).
 // Pipelining: the next block's K/V are loaded global -> registers while the current block
 // computes, then written to the other LDS buffer; one workgroup barrier per block.  The
 // sequence's block-table slice is staged in LDS once so K/V addresses need no dependent
@@ -34,11 +35,18 @@ constexpr int kD = 128;
 constexpr int kNS = 2;                   // 32-key sub-tiles per block
 constexpr int kKB = 32 * kNS;            // keys per block
 constexpr int kKStride = kD + 8;         // K tile row: 272 B (16 B reads conflict-free)
-constexpr int kVStride = kKB + 4;        // V^T tile row: 136 B (8 B reads conflict-free)
+// V^T tile row: 144 B (16-B aligned rows; 36-dword stride: the PV operand's ds_read_b128 and
+// the staging ds_write_b64 pairs are bank-conflict-free).  Inside every 16-key group the keys
+// are stored permuted - key 8 a + 4 h + b at column 8 h + 4 a + b - so the 8 keys one lane
+// needs for a PV fragment (keys 4 h .. 4 h + 3 and 8 + 4 h .. 8 + 4 h + 3, the order of the P^T
+// registers) are one contiguous 16 B read: one ds_read_b128 (4 LDS cycles) instead of a
+// ds_read2_b64 (8).
+constexpr int kVStride = kKB + 8;
 constexpr int kKTile = kKB * kKStride;   // elements
 constexpr int kVTile = kD * kVStride;
 constexpr int kBtLds = 2048;             // block-table entries staged in LDS
 constexpr float kNegInf = -__builtin_huge_valf();
+constexpr float kRescale = 8.f;  // defer-max threshold (log2 units)
 
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
@@ -76,9 +84,24 @@ struct FlashParams {
   float scale_log2;
 };
 
+// two floats -> one packed 16-bit pair.  bf16: a single v_cvt_pk_bf16_f32 (RNE); element-wise
+// conversion compiled to 2 converts + shift + or per pair, 64 VALU per block per wave.
 template <typename T>
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return static_cast<uint32_t>(from_f32<T>(a)) | (static_cast<uint32_t>(from_f32<T>(b)) << 16);
+}
+template <>
+__device__ __forceinline__ uint32_t pack2<__bf16>(float a, float b) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{a, b}), bf16x2_t));
+}
+
+// lane l <-> lane l ^ 32 exchange: one ds_bpermute with the byte index hoisted out of the loop
+// (__shfl_xor recomputed it per call: 7 VALU).  Not v_permlane32_swap: with both operands the
+// same value the compiler folded its two results into one (sum -> 2 * r0), a wrong softmax sum.
+__device__ __forceinline__ float xor32(float v, int idx4) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(idx4, __builtin_bit_cast(int, v)));
 }
 
 template <typename T, int G>
@@ -93,9 +116,10 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wid = tid >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform -> SGPR
   const int r = lane & 31;   // column within the wave / row within a 32-row operand
   const int h = lane >> 5;   // lane half
+  const int x32 = (lane ^ 32) << 2;  // ds_bpermute byte index of the partner lane
   // 1-D grid, KV head fastest: blocks are dealt round-robin over the 8 XCDs, so with 8 KV
   // heads every tile of head hk runs on one XCD and the head's K/V (re-read by all its
   // tiles) stays in that XCD's L2 instead of being pulled into all eight (placement is a
@@ -144,51 +168,52 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
   __syncthreads();  // lds_bt ready
 
   // ---- global -> register staging of one K/V block --------------------------------------
-  // K tile: kKB x 16 chunks of 16 B, chunk c = (key c >> 4, dims 8 (c & 15));
-  // V^T tile: 128 x kKB / 8 chunks, chunk c = (d c / (kKB / 8), keys 8 (c % (kKB / 8)));
-  // thread t handles chunks t + 256 u
+  // Wave w stages keys 16 w .. 16 w + 15 of the block for BOTH tensors: with BS >= 16 those
+  // keys sit in one page, so the page lookup is wave-uniform (one LDS read + readfirstlane,
+  // a scalar base) and every lane offset is a loop constant - the per-lane 64-bit address
+  // arithmetic of 8 independent lookups was ~70 VALU per block and wave.
+  //   K: lane l, chunk u -> key row 16 w + 4 u + (l >> 4), dims 8 (l & 15): each
+  //      instruction reads 4 contiguous 256 B rows (1 KiB);
+  //   V: lane l, chunk u -> d-row 32 u + (l >> 1), keys 16 w + 8 (l & 1) .. + 7: each
+  //      instruction reads 32 d-rows x 16 keys (1 KiB contiguous at BS = 16).
   constexpr int kChunks = kKB * 16 / 256;   // per thread, per tensor
-  constexpr int kVq = kKB / 8;              // 8-key groups per V^T row
+  static_assert(kKB == 64 && kChunks == 4, "wave w stages keys 16 w .. 16 w + 15");
+  const int pshift = p.bs_shift + 7;        // log2(BS * kD) elements per (page, head)
+  const int last_page = npages - 1;
+  const int w_keyoff = (16 * wid) & (BS - 1);               // wave's first key in its page
+  const int k_lane = (lane >> 4) * kD + 8 * (lane & 15) + w_keyoff * kD;
+  const int v_lane = (lane >> 1) * BS + 8 * (lane & 1) + w_keyoff;
+  const int k_lds = (16 * wid + (lane >> 4)) * kKStride + 8 * (lane & 15);
+  const int v_lds = (lane >> 1) * kVStride + 16 * wid + 4 * (lane & 1);  // permuted: see kVStride
   // LDS only (the launcher rejects bt_stride > kBtLds): a select between the LDS copy and the
   // global table compiled to FLAT loads, whose vmcnt wait put a dependent global round trip
-  // in front of every block's K/V loads
-  auto page_of = [&](int key) -> int { return lds_bt[key >> p.bs_shift]; };
-  const int64_t head_elems = static_cast<int64_t>(BS) * kD;  // per (page, head)
+  // in front of every block's K/V loads.  Keys past the causal range read a clamped (valid,
+  // finite: the cache is zero-initialised and only ever holds real tokens) page; their
+  // scores are masked and their P is 0.
   u32x4 kr[kChunks], vr[kChunks];
   auto load_block = [&](int kb) {
+    const int pi = min((kb * kKB + 16 * wid) >> p.bs_shift, last_page);
+    const int pg = __builtin_amdgcn_readfirstlane(lds_bt[pi]);
+    const uint64_t off = static_cast<uint64_t>(static_cast<uint32_t>(pg * p.n_kv_heads + hk)) << pshift;
+    const uint16_t* kb_ = p.k_cache + off;
+    const uint16_t* vb_ = p.v_cache + off;
 #pragma unroll
-    for (int u = 0; u < kChunks; ++u) {
-      const int c = tid + 256 * u;
-      int key = kb * kKB + (c >> 4);
-      key = min(key, wg_end - 1);  // rows past the causal range are masked; stay in-table
-      const int pg = page_of(key);
-      const uint16_t* src = p.k_cache + (static_cast<int64_t>(pg) * p.n_kv_heads + hk) * head_elems +
-                            static_cast<int64_t>(key & (BS - 1)) * kD + 8 * (c & 15);
-      kr[u] = *reinterpret_cast<const u32x4*>(src);
-    }
+    for (int u = 0; u < kChunks; ++u)
+      kr[u] = *reinterpret_cast<const u32x4*>(kb_ + k_lane + u * 4 * kD);
 #pragma unroll
-    for (int u = 0; u < kChunks; ++u) {
-      const int c = tid + 256 * u;
-      int key = kb * kKB + 8 * (c % kVq);
-      key = min(key, (wg_end - 1) & ~7);  // 8-key groups never straddle a page (BS >= 16)
-      const int pg = page_of(key);
-      const uint16_t* src = p.v_cache + (static_cast<int64_t>(pg) * p.n_kv_heads + hk) * head_elems +
-                            static_cast<int64_t>(c / kVq) * BS + (key & (BS - 1));
-      vr[u] = *reinterpret_cast<const u32x4*>(src);
-    }
+    for (int u = 0; u < kChunks; ++u)
+      vr[u] = *reinterpret_cast<const u32x4*>(vb_ + v_lane + u * 32 * BS);
   };
   auto store_block = [&](int buf) {
 #pragma unroll
-    for (int u = 0; u < kChunks; ++u) {
-      const int c = tid + 256 * u;
-      *reinterpret_cast<u32x4*>(&lds_k[buf][(c >> 4) * kKStride + 8 * (c & 15)]) = kr[u];
-    }
+    for (int u = 0; u < kChunks; ++u)
+      *reinterpret_cast<u32x4*>(&lds_k[buf][k_lds + u * 4 * kKStride]) = kr[u];
 #pragma unroll
     for (int u = 0; u < kChunks; ++u) {
-      const int c = tid + 256 * u;
-      uint16_t* dst = &lds_v[buf][(c / kVq) * kVStride + 8 * (c % kVq)];  // 8 B aligned rows
+      // keys 8 g .. 8 g + 3 -> columns 4 g .., keys 8 g + 4 .. 8 g + 7 -> columns 8 + 4 g ..
+      uint16_t* dst = &lds_v[buf][v_lds + u * 32 * kVStride];
       reinterpret_cast<u32x2*>(dst)[0] = u32x2{vr[u][0], vr[u][1]};
-      reinterpret_cast<u32x2*>(dst)[1] = u32x2{vr[u][2], vr[u][3]};
+      reinterpret_cast<u32x2*>(dst + 8)[0] = u32x2{vr[u][2], vr[u][3]};
     }
   };
 
@@ -232,43 +257,60 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
       // vmcnt(0) for them: every block paid the whole load latency.
       if (more) load_block(kb + 1);
       issued = true;
-      // mask (only blocks crossing the diagonal of the wave's first token, or kvlen)
-      const bool need_mask = k0 + kKB > ctx0 + w_first + 1;
+      // mask: only blocks crossing the diagonal of the wave's first token (wave-uniform
+      // branch); element (t, i) holds key k0 + 4 h + 32 t + (i & 3) + 8 (i >> 2), a compile-
+      // time offset from the lane's base, so a compare with one per-lane limit suffices
+      if (k0 + kKB > ctx0 + w_first + 1) {
+        const int lim = c_end - k0 - 4 * h;
+#pragma unroll
+        for (int t = 0; t < kNS; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (32 * t + (i & 3) + 8 * (i >> 2) >= lim) sacc[t][i] = kNegInf;
+      }
+      // running max on the raw scores (scale > 0), softmax in the log2 domain with the scale
+      // folded into one fma per element: p = 2^(s * scale_log2 - m)
       float tmax = kNegInf;
 #pragma unroll
       for (int t = 0; t < kNS; ++t)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int key = k0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
-          float v = sacc[t][i] * p.scale_log2;
-          if (need_mask && key >= c_end) v = kNegInf;
-          sacc[t][i] = v;
-          tmax = fmaxf(tmax, v);
-        }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, kWave));
-      const float m_new = fmaxf(m_run, tmax);
-      const float m_use = (m_new == kNegInf) ? 0.f : m_new;
-      // rescale O only when some column's running max moved (wave-uniform skip: after the
-      // first blocks the max rarely changes)
-      if (__any(m_new != m_run)) {
-        const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
+        for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, sacc[t][i]);
+      tmax = fmaxf(tmax, xor32(tmax, x32));
+      // defer-max (guide §5.5 T13): the running max m_run moves only when some column's max
+      // grew by more than kRescale (log2 units), so P = 2^(s - m_run) stays <= 2^kRescale;
+      // O and l are rescaled only then - with the max nearly settled after the first block,
+      // the 32 packed multiplies of the rescale were paid on most blocks.  O, l and P of a
+      // block always use the same m_run, so the result is exact up to rounding.
+      const float m_cand = fmaxf(m_run, tmax * p.scale_log2);
+      const bool grow = m_cand > m_run + kRescale;  // m_run == -inf: any finite m_cand
+      if (__any(grow)) {
+        const float m_new = grow ? m_cand : m_run;
+        const float alpha = __builtin_amdgcn_exp2f(m_run - ((m_new == kNegInf) ? 0.f : m_new));
         l_run *= alpha;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
           for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+        m_run = m_new;
       }
-      m_run = m_new;
-      float psum = 0.f;
+      const float m_use = (m_run == kNegInf) ? 0.f : m_run;
+      // exponent arguments and the row sum on packed f32 pairs (v_pk_fma_f32 / v_pk_add_f32)
+      typedef float f32x2_t __attribute__((ext_vector_type(2)));
+      const f32x2_t sc2 = {p.scale_log2, p.scale_log2};
+      const f32x2_t nm2 = {-m_use, -m_use};
+      f32x2_t ps2 = {0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < kNS; ++t)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float e = __builtin_amdgcn_exp2f(sacc[t][i] - m_use);
-          sacc[t][i] = e;
-          psum += e;
+        for (int i = 0; i < 16; i += 2) {
+          const f32x2_t a = __builtin_elementwise_fma(f32x2_t{sacc[t][i], sacc[t][i + 1]}, sc2, nm2);
+          const f32x2_t e = {__builtin_amdgcn_exp2f(a[0]), __builtin_amdgcn_exp2f(a[1])};
+          sacc[t][i] = e[0];
+          sacc[t][i + 1] = e[1];
+          ps2 += e;
         }
-      psum += __shfl_xor(psum, 32, kWave);
+      float psum = ps2[0] + ps2[1];
+      psum += xor32(psum, x32);
       l_run += psum;
       // P^T fragments per 16-key step: registers 8s..8s+7 of the sub-tile packed pairwise;
       // O^T += V^T . P^T (A element j of half h = key 16 s + 8 (j >> 2) + 4 h + (j & 3))
@@ -285,12 +327,10 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
         }
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
-          const uint16_t* vrow = vl + (32 * dt + r) * kVStride + 32 * t + 4 * h;
+          const uint16_t* vrow = vl + (32 * dt + r) * kVStride + 32 * t + 8 * h;
 #pragma unroll
           for (int st = 0; st < 2; ++st) {
-            const u32x2 lo = *reinterpret_cast<const u32x2*>(vrow + 16 * st);
-            const u32x2 hi = *reinterpret_cast<const u32x2*>(vrow + 16 * st + 8);
-            const frag vf = __builtin_bit_cast(frag, u32x4{lo[0], lo[1], hi[0], hi[1]});
+            const frag vf = *reinterpret_cast<const frag*>(vrow + 16 * st);
             o[dt] = MF::mma(vf, pf[st], o[dt]);
           }
         }

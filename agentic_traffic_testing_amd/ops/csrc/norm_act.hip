@@ -77,23 +77,29 @@ __global__ __launch_bounds__(kNormThreads) void rms_norm_kernel(
 // weight is loaded together with x (one memory round trip instead of two) - the prefill norm
 // at 2.6k rows x 4096 ran at 2.6 TB/s as one 256-thread workgroup per row.  Same per-element
 // arithmetic as rms_norm_kernel (only the fp32 summation order of the row sum differs).
+// WPR > 1 (few rows: the burst / planning prefills, 73-382 rows) spreads a row over WPR waves
+// so the launch has 4x the waves in flight; the partial sums of squares meet in LDS behind one
+// barrier.  At 382 x 4096 the one-wave-per-row form ran 10.5 us (1.2 TB/s: 96 workgroups).
 constexpr int kRowsPerWg = 4;
-template <typename T, bool kAdd, int ITERS>
-__global__ __launch_bounds__(64 * kRowsPerWg) void rms_norm_wave_kernel(
+constexpr int kNormSmallRows = 1024;  // below: 4 waves per row
+template <typename T, bool kAdd, int ITERS, int WPR = 1>
+__global__ __launch_bounds__(256) void rms_norm_wave_kernel(
     uint16_t* __restrict__ out, uint16_t* __restrict__ residual, const uint16_t* __restrict__ x,
     const uint16_t* __restrict__ w, int rows, int hidden, int64_t x_stride, int64_t out_stride,
     int64_t res_stride, float eps) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = static_cast<int64_t>(blockIdx.x) * kRowsPerWg + (threadIdx.x >> 6);
-  if (row >= rows) return;  // wave-uniform; no block-level barrier below
-  const int nvec = hidden >> 3;
+  constexpr int kRows = 4 / WPR;  // rows per 256-thread workgroup
+  const int lane = threadIdx.x & (64 * WPR - 1);
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kRows + threadIdx.x / (64 * WPR);
+  if (WPR == 1 && row >= rows) return;  // wave-uniform; no block-level barrier below
+  const bool live = row < rows;         // WPR > 1: every wave reaches the barrier
+  const int nvec = live ? hidden >> 3 : 0;
   const Pack8* xin = reinterpret_cast<const Pack8*>(x + row * x_stride);
   Pack8* rrow = kAdd ? reinterpret_cast<Pack8*>(residual + row * res_stride) : nullptr;
   const Pack8* wv = reinterpret_cast<const Pack8*>(w);
   Pack8 xa[ITERS], wa[ITERS], ra[ITERS];
 #pragma unroll
   for (int it = 0; it < ITERS; ++it) {
-    const int v = lane + it * 64;
+    const int v = lane + it * 64 * WPR;
     if (v < nvec) {
       xa[it] = xin[v];
       wa[it] = wv[v];
@@ -104,7 +110,7 @@ __global__ __launch_bounds__(64 * kRowsPerWg) void rms_norm_wave_kernel(
   float ss = 0.f;
 #pragma unroll
   for (int it = 0; it < ITERS; ++it) {
-    const int v = lane + it * 64;
+    const int v = lane + it * 64 * WPR;
     if (v < nvec) {
       if constexpr (kAdd) {
         Pack8 s;
@@ -123,11 +129,21 @@ __global__ __launch_bounds__(64 * kRowsPerWg) void rms_norm_wave_kernel(
     }
   }
   ss = wave_sum(ss);
+  if constexpr (WPR > 1) {
+    __shared__ float part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    const int w0 = (threadIdx.x >> 6) & ~(WPR - 1);
+    ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < WPR; ++i) ss += part[w0 + i];  // same order in every wave of the row
+    if (!live) return;
+  }
   const float inv = rsqrtf(ss / static_cast<float>(hidden) + eps);
   Pack8* o = reinterpret_cast<Pack8*>(out + row * out_stride);
 #pragma unroll
   for (int it = 0; it < ITERS; ++it) {
-    const int v = lane + it * 64;
+    const int v = lane + it * 64 * WPR;
     if (v < nvec) {
       Pack8 r;
 #pragma unroll
@@ -239,6 +255,25 @@ int atta_rms_norm(void* out, void* residual, const void* x, const void* w, int r
   auto xi = static_cast<const uint16_t*>(x);
   auto wi = static_cast<const uint16_t*>(w);
   const int iters = (hidden / 8 + 63) / 64;
+  if (iters <= 16 && rows < kNormSmallRows) {
+    // few rows: 4 waves per row, one row per workgroup
+    const dim3 g2(rows), b2(256);
+#define ATTA_RMSW(T_, ADD_, IT_)                                                                   \
+  rms_norm_wave_kernel<T_, ADD_, IT_, 4><<<g2, b2, 0, stream>>>(o, r, xi, wi, rows, hidden, x_stride, \
+                                                                out_stride, res_stride, eps)
+#define ATTA_RMSW_IT(T_, ADD_)                 \
+  if (iters <= 4) ATTA_RMSW(T_, ADD_, 1);      \
+  else if (iters <= 8) ATTA_RMSW(T_, ADD_, 2); \
+  else ATTA_RMSW(T_, ADD_, 4)
+    if (dtype == 0) {
+      if (r) { ATTA_RMSW_IT(__bf16, true); } else { ATTA_RMSW_IT(__bf16, false); }
+    } else {
+      if (r) { ATTA_RMSW_IT(_Float16, true); } else { ATTA_RMSW_IT(_Float16, false); }
+    }
+#undef ATTA_RMSW_IT
+#undef ATTA_RMSW
+    return static_cast<int>(hipGetLastError());
+  }
   if (iters <= 16) {
     const dim3 g2((rows + kRowsPerWg - 1) / kRowsPerWg), b2(64 * kRowsPerWg);
 #define ATTA_RMSW(T_, ADD_, IT_)                                                                \

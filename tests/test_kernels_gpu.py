@@ -166,6 +166,24 @@ def test_flash_prefill_long_chunked(hq, hkv):
     close(got, exp, 1.5e-2, 2e-2)
 
 
+@pytest.mark.parametrize("qscale", [6.0, 24.0])
+@pytest.mark.parametrize("bs", [16, 32])
+def test_flash_prefill_large_logits(qscale, bs):
+    """Scores spread over tens of log2 units, so running maxima keep growing past the
+    defer-max threshold: the kernel's rescale of O and l (taken only when a column's max grew
+    by more than 2^8) and its stale-max blocks must still match the fp32 reference."""
+    torch.manual_seed(7)
+    dt = torch.bfloat16
+    seqs = [(700, 700), (1500, 400)]
+    k, v, bt, kvlen, qstart, T = _make_paged(seqs, 8, bs, dt)
+    q = (torch.randn(T, 32, 128, device="cuda") * qscale).to(dt)
+    ts, to = _tiles(seqs, ops.prefill_tile_tokens(4, "flash"))
+    scale = 1 / math.sqrt(128)
+    exp = ref.paged_attention(q, k, v, bt.clamp(min=0), kvlen, qstart, scale)
+    got = ops.attention_prefill(q, k, v, bt, kvlen, qstart, ts, to, scale, impl="flash")
+    close(got, exp, 1.5e-2, 2e-2)
+
+
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 1), (4, 1), (24, 8)])
 @pytest.mark.parametrize("parts", [1, 4, 16])
