@@ -225,6 +225,12 @@ FLASH_MAX_BT = 2048
 
 
 def prefill_impl(bt_width: int = 0, impl: str | None = None) -> str:
+    """The prefill attention kernel for block tables of ``bt_width`` entries: the configured
+    default falls back to v1 past FLASH_MAX_BT; an explicit "flash" there is an error (the
+    caller's tiles would not match the kernel that runs)."""
+    if impl == "flash" and bt_width > FLASH_MAX_BT:
+        raise ValueError(f"flash prefill stages at most {FLASH_MAX_BT} block-table entries "
+                         f"per sequence (got {bt_width}); use impl=None or 'v1'")
     impl = impl or PREFILL_IMPL
     return "v1" if impl == "flash" and bt_width > FLASH_MAX_BT else impl
 

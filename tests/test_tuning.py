@@ -45,3 +45,19 @@ def _gen(pad: bool):
 
 def test_padded_prefill_matches_unpadded():
     assert _gen(True) == _gen(False)
+
+
+def test_prefill_impl_falls_back_past_flash_table_width():
+    """The flash prefill kernel stages a sequence's whole block-table row in LDS: wider tables
+    take v1 by default (tile size and kernel chosen together), an explicit flash request fails."""
+    import pytest
+
+    from agentic_traffic_testing_amd import ops
+
+    assert ops.prefill_impl(ops.FLASH_MAX_BT, None) == ops.PREFILL_IMPL
+    if ops.PREFILL_IMPL == "flash":
+        assert ops.prefill_impl(ops.FLASH_MAX_BT + 1, None) == "v1"
+        assert ops.prefill_tile_tokens(4, bt_width=ops.FLASH_MAX_BT + 1) == \
+            ops.prefill_tile_tokens(4, "v1")
+    with pytest.raises(ValueError):
+        ops.prefill_impl(ops.FLASH_MAX_BT + 1, "flash")
