@@ -218,6 +218,9 @@ class EngineConfig:
     # the measured A/B at that size: models/llama.py LlamaModel._PG_AUTO)
     prefill_gemm: str = "auto"
     prefill_gemm_min_rows: int = 128
+    # prefill steps of <= 32 rows (cached-prompt planning prefills, short chunks) on the fused
+    # decode kernels (norm-folded skinny GEMVs, RoPE / KV write / SiLU epilogues)
+    small_prefill_fused: bool = True
     # library prefill GEMMs from a TunableOp solution table (rocBLAS / hipBLASLt solution per
     # exact shape, tuned cold on MI355X by scripts/gpu/tune_prefill_gemms.py): "auto" = the
     # table shipped for this GPU (agentic_traffic_testing_amd/tuning/), "" = off, else a path.

@@ -119,6 +119,7 @@ class ModelRunner:
                                 quantization=cfg.quantization)
         self.model.prefill_gemm = cfg.prefill_gemm
         self.model.prefill_gemm_min_rows = cfg.prefill_gemm_min_rows
+        self.model.small_prefill_fused = cfg.small_prefill_fused
         # tuned library-GEMM table (agentic_traffic_testing_amd/tuning): prefill steps pad
         # their rows to its buckets so their GEMMs hit tuned shapes
         self.gemm_table = None

@@ -88,6 +88,8 @@ class LlamaModel:
         # hand-written CDNA4 GEMM, ops/csrc/prefill_gemm.hip) for >= prefill_gemm_min_rows rows
         self.prefill_gemm = "auto"
         self.prefill_gemm_min_rows = 128
+        # prefill steps of <= 32 rows on the fused decode kernels (EngineConfig.small_prefill_fused)
+        self.small_prefill_fused = True
         self.cfg = cfg
         self.dtype = dtype
         self.device = torch.device(device)
@@ -316,8 +318,21 @@ class LlamaModel:
         fp8 = self.quant == "fp8" and self.device.type == "cuda"
         dt = residual.dtype
         pending = None  # fp8: the previous down_proj output, added by the next norm kernel
+        # small steps (<= 32 rows: cached-prompt planning prefills, short chunks) run the fused
+        # decode kernels - RMSNorm folded into the skinny GEMVs over the pre-shuffled weights,
+        # RoPE + KV write in the QKV epilogue, SiLU-mul in gate_up - around the prefill
+        # attention: 5 launches per layer at weight-stream speed instead of ~9 with the
+        # row-major skinny / library GEMMs (17 rows: 168 -> ~80 us of GEMMs per layer,
+        # profiles/r4_small_prefill_fused.txt)
+        small = (self.small_prefill_fused and self.device.type == "cuda" and self.tp_size == 1
+                 and not fp8 and T <= ops.SKINNY_MAX_M and self.decode_fusable(T))
         for li, L in enumerate(self.layers):
-            if fp8:
+            ps = L.qkv_ps is not None
+            if small:
+                q = ops.decode_qkv_rope(residual, L.qkv_ps if ps else L.qkv, eps, md.positions,
+                                        md.slot_mapping, self.cos_sin, k_caches[li],
+                                        v_caches[li], nq, nkv, preshuffled=ps)
+            elif fp8:
                 if pending is None:
                     xq, xs = ops.quant_rows_fp8(residual, ops.QUANT_NORM, L.input_norm, eps)
                 else:
@@ -328,8 +343,9 @@ class LlamaModel:
                 qkv = ops.prefill_gemm(ops.rms_norm(residual, L.input_norm, eps), L.qkv)
             else:
                 qkv = self._proj(ops.rms_norm(residual, L.input_norm, eps), L.qkv, L.qkv_s)
-            q = ops.rope_cache(qkv, md.positions, md.slot_mapping, self.cos_sin, k_caches[li],
-                               v_caches[li], nq, nkv, D)
+            if not small:
+                q = ops.rope_cache(qkv, md.positions, md.slot_mapping, self.cos_sin,
+                                   k_caches[li], v_caches[li], nq, nkv, D)
             attn = torch.empty_like(q)
             if md.num_decode > 0:
                 ops.attention_decode(q, k_caches[li], v_caches[li], md.block_tables,
@@ -351,6 +367,16 @@ class LlamaModel:
                     gu = ops.gemm_fp8(xq, xs, L.gate_up, L.gate_up_s, dt)
                     aq, as_ = ops.quant_rows_fp8(gu, ops.QUANT_SILU)
                 pending = self._all_reduce(self._gemm8(aq, as_, L.down, L.down_s, dt, "down"))
+                continue
+            if small:
+                ops.linear(attn.view(T, nq * D), L.o_ps if ps else L.o, residual=residual,
+                           waves=ops.decode_waves("o", ps, False), preshuffled=ps, ksplit=None,
+                           proj="o")
+                a = ops.decode_gate_up_silu(residual, L.gate_up_ps if ps else L.gate_up, eps,
+                                            preshuffled=ps)
+                ops.linear(a, L.down_ps if ps else L.down, residual=residual,
+                           waves=ops.decode_waves("down", ps, False), preshuffled=ps,
+                           ksplit=None, proj="down")
                 continue
             self._proj_residual(attn.view(T, nq * D), L.o, L.o_s, residual, "o")
             x = ops.rms_norm(residual, L.post_norm, eps)
