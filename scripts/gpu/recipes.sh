@@ -1,0 +1,67 @@
+#!/bin/bash
+# Named GPU-box recipes over scripts/gpu/stages.sh (one per measurement this repo's profiles
+# cite).  Every step runs under its own time limit; the first failure ends the call.
+#
+#   bash scripts/gpu/recipes.sh final          # pytest -m gpu, smoke, bench, windowed profiles
+#   bash scripts/gpu/recipes.sh <name> [...]   # several recipes in order
+#
+# Recipes (profiles they produced in round 4):
+#   final        tests + smoke + 5-step bench + profbench + 3092-token prefill profile
+#                (r4_final_gpu_tier.log, r4_final_profbench_summary.txt, r4_prof_prefill3k_after_summary.txt)
+#   driverlike   bench.py --gpus 1 --steps 20 --warmup 5, the driver's invocation (r4_driverlike_bench.log)
+#   refresh      HTTP fan-out, 8B fp8, 70B fp8 TP=1 benches (r4_final_secondary.log)
+#   tp8          TP=8 rehearsal (8 ranks on one GPU) with graph node dumps, push on / off, and the
+#                AgentVerse HTTP runs on 8B and 70B fp8 (r4_tp8_*, r4_http_agentverse_*)
+#   largem       large-M GEMM routing A/B vs the tuned library table (r4_prefill_gemm_largem_ab.txt)
+#   flash        flash-prefill tests, microbench, elementwise probe, PMC passes (r4_flash_prefill_rework.txt)
+#   burst        windowed profile of the 380-row burst prefill (r4_prof_burst380_summary.txt)
+#   small        17 / 85-row prefill profiles and the cached-regime bench with the fused small-prefill
+#                path on / off (r4_small_prefill_fused.txt)
+set -u -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+S=scripts/gpu/stages.sh
+recipe() {
+  case $1 in
+    final)
+      TAG=r4final STAGES="tests smoke bench profbench" STEPS=${STEPS:-5} TEST_TIMEOUT=1000 bash $S &&
+      TAG=r4finalpf3k STAGES=profpf TOKENS=3092 SEQS=1 bash $S ;;
+    driverlike)
+      timeout -k 10 900 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r4_driverlike_bench.log 2>&1 &&
+      tail -1 gpurun_out/r4_driverlike_bench.log ;;
+    refresh)
+      TAG=r4fin STAGES=http STEPS=3 bash $S &&
+      TAG=r4fin_fp8 STAGES=bench STEPS=2 BENCH_ARGS="--quantization fp8" bash $S &&
+      TAG=r4fin_70bfp8 STAGES=bench STEPS=1 BENCH_ARGS="--model llama-3-70b --quantization fp8" bash $S ;;
+    tp8)
+      local tp="--gpus 8 --parallel tp --tp-same-device --model llama-70b-tp-slice --max-tokens 64"
+      ATTA_GRAPH_DUMP_DIR=gpurun_out/graphs_push TAG=r4tp8push STAGES=bench STEPS=1 BENCH_ARGS="$tp" bash $S &&
+      python scripts/gpu/graph_nodes.py gpurun_out/graphs_push > gpurun_out/r4_tp8_graph_nodes.txt &&
+      ATTA_GRAPH_DUMP_DIR=gpurun_out/graphs_nopush TAG=r4tp8nopush STAGES=bench STEPS=1 \
+        BENCH_ARGS="$tp --set tp_fused_push=0" bash $S &&
+      python scripts/gpu/graph_nodes.py gpurun_out/graphs_nopush > gpurun_out/r4_tp8_graph_nodes_nopush.txt &&
+      rm -rf gpurun_out/graphs_push gpurun_out/graphs_nopush &&
+      TAG=r4av8b STAGES=http STEPS=1 BENCH_ARGS="--workload agentverse" bash $S &&
+      TAG=r4av70b STAGES=http STEPS=1 BENCH_ARGS="--workload agentverse --model llama-3-70b --quantization fp8" bash $S ;;
+    largem)
+      TAG=r4lm_bf16 STAGES=gemm GEMM_ARGS="--m 2048 2560 3200 4096 --tuned auto --rounds 3" bash $S &&
+      TAG=r4lm_fp8 STAGES=gemm GEMM_ARGS="--m 512 1024 2048 3200 --fp8 --rounds 3" bash $S ;;
+    flash)
+      TAG=r4fa STAGES=tests PYTEST_ARGS="tests/test_kernels_gpu.py" PYTEST_K="prefill or flash or long or norm" \
+        TEST_TIMEOUT=400 bash $S &&
+      TAG=r4fa STAGES=py PY_ARGS="scripts/gpu/microbench_prefill_attn.py --impls flash" PY_TIMEOUT=300 bash $S &&
+      TAG=r4faew STAGES=py PY_ARGS="scripts/gpu/probe_elementwise.py --m 73 382 3200" PY_TIMEOUT=200 bash $S &&
+      bash scripts/gpu/run_r4_fa_pmc.sh ;;
+    burst)
+      TAG=r4burst STAGES=profpf TOKENS=380 SEQS=5 REPS=5 bash $S ;;
+    small)
+      TAG=r4sp17 STAGES=profpf TOKENS=17 SEQS=1 REPS=10 bash $S &&
+      TAG=r4sp85 STAGES=profpf TOKENS=85 SEQS=5 REPS=10 bash $S &&
+      TAG=r4sf_on STAGES=bench STEPS=6 BENCH_ARGS="--warmup 5" bash $S &&
+      TAG=r4sf_off STAGES=bench STEPS=6 BENCH_ARGS="--warmup 5 --set small_prefill_fused=0" bash $S ;;
+    *) echo "unknown recipe $1"; return 2 ;;
+  esac
+}
+for r in "${@:-final}"; do
+  echo "### recipe $r"
+  recipe "$r" || { echo "STOP after recipe $r"; exit 1; }
+done
