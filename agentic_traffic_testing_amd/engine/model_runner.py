@@ -137,6 +137,10 @@ class ModelRunner:
                              or cfg.quantization == "fp8"):
             self.model.prepare_decode_weights()
         self.load_seconds = time.perf_counter() - t0
+        if self.is_cuda:
+            # split-K GEMV workspace up front (32 MiB): a split chosen while a decode graph is
+            # being captured (ATTA_DECODE_KSPLIT, TP shards) must not allocate inside the capture
+            ops.ensure_splitk_workspace(self.device)
         self.block_size = cfg.block_size
         self.bt_width = math.ceil(cfg.max_model_len / cfg.block_size)
         self.part_tokens = cfg.decode_partition_tokens
