@@ -332,7 +332,15 @@ for _item in filter(None, os.environ.get("ATTA_DECODE_WAVES", "").split(",")):
     DECODE_WAVES[_proj][_fmt] = int(_val)
 
 
-def decode_waves(proj: str, preshuffled: bool = False, fp8: bool = False) -> int:
+# 17-32 rows (two MFMA row blocks: the fused small-prefill path) stream gate_up best with 8
+# waves - half the per-workgroup cross-wave reduction per weight byte: 71.8 -> 59.2 us at 17
+# rows, while 16 waves stay best at <= 16 rows (profiles/r4_skinny_mt_probe.txt)
+DECODE_WAVES_MT2 = {"gate_up": 8}
+
+
+def decode_waves(proj: str, preshuffled: bool = False, fp8: bool = False, m: int = 0) -> int:
+    if m > 16 and preshuffled and not fp8 and proj in DECODE_WAVES_MT2:
+        return DECODE_WAVES_MT2[proj]
     return DECODE_WAVES[proj]["fp8" if fp8 else ("ps" if preshuffled else "rm")]
 
 
@@ -699,7 +707,7 @@ def decode_gate_up_silu(x, w, eps, out=None, preshuffled=False, w_scale=None, ks
         n = ref.rms_norm(x, torch.ones(x.shape[1], dtype=x.dtype), eps)
         out.copy_(ref.silu_and_mul(torch.nn.functional.linear(n, w)))
         return out
-    waves = decode_waves("gate_up", preshuffled, w_scale is not None)
+    waves = decode_waves("gate_up", preshuffled, w_scale is not None, m=x.shape[0])
     _native().fused_gate_up_silu(out, x, w, eps, waves, preshuffled or w_scale is not None,
                                  w_scale, _ksplit("gate_up", x, ksplit, w.shape[0] // 16))
     return out

@@ -1,0 +1,43 @@
+"""Why a 17-row step of the fused decode GEMVs costs ~1.8x a 16-row one (gate_up 69 vs 39 us):
+times ops.decode_gate_up_silu on the pre-shuffled 8B gate_up at M = 8, 16, 17, 24, 32 (cold
+weights: rotating copies), for a PMC pass with --only-m.
+
+    python scripts/gpu/probe_skinny_mt.py [--only-m 17]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+from agentic_traffic_testing_amd import ops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only-m", type=int, default=0)
+    a = ap.parse_args()
+    n, k = 28672, 4096
+    copies = 4
+    ws = [ops.preshuffle((torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16), "silu")
+          for _ in range(copies)]
+    for m in ([a.only_m] if a.only_m else [8, 16, 17, 24, 32]):
+        x = torch.randn(m, k, device="cuda").to(torch.bfloat16)
+        out = torch.empty(m, n // 2, device="cuda", dtype=torch.bfloat16)
+        for i in range(3):
+            ops.decode_gate_up_silu(x, ws[i % copies], 1e-5, out=out, preshuffled=True)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        iters = 40
+        for i in range(iters):
+            ops.decode_gate_up_silu(x, ws[i % copies], 1e-5, out=out, preshuffled=True)
+        e1.record()
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) * 1e3 / iters
+        print(f"gate_up+silu M={m:3d}: {t:7.1f} us ({n * k * 2 / t / 1e6:5.2f} TB/s)", flush=True)
+
+
+if __name__ == "__main__":
+    main()
