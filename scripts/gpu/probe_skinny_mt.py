@@ -14,10 +14,42 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
 from agentic_traffic_testing_amd import ops  # noqa: E402
 
 
+def sweep_linear():
+    """waves sweep for the residual-epilogue projections (o, down; qkv as a plain GEMV) at
+    1-2 MFMA row blocks, pre-shuffled bf16 8B shapes, cold weights."""
+    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "down": (4096, 14336)}
+    for proj, (n, k) in shapes.items():
+        ws = [ops.preshuffle((torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16))
+              for _ in range(4)]
+        for m in (16, 17, 32):
+            x = torch.randn(m, k, device="cuda").to(torch.bfloat16)
+            res = torch.zeros(m, n, device="cuda", dtype=torch.bfloat16)
+            row = []
+            for waves in (4, 8, 16):
+                def run(i):
+                    ops.linear(x, ws[i % 4], residual=res, waves=waves, preshuffled=True,
+                               ksplit=None, proj=proj)
+                for i in range(3):
+                    run(i)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for i in range(40):
+                    run(i)
+                e1.record()
+                torch.cuda.synchronize()
+                row.append(f"w{waves}={e0.elapsed_time(e1) * 1e3 / 40:6.1f}us")
+            print(f"{proj:5s} M={m:3d}: " + "  ".join(row), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only-m", type=int, default=0)
+    ap.add_argument("--sweep-linear", action="store_true")
     a = ap.parse_args()
+    if a.sweep_linear:
+        sweep_linear()
+        return
     n, k = 28672, 4096
     copies = 4
     ws = [ops.preshuffle((torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16), "silu")
