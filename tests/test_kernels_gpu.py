@@ -553,6 +553,7 @@ def test_preshuffled_decode_kernels_bit_identical(m, monkeypatch):
     monkeypatch.setattr(ops, "DECODE_WAVES",
                         {k: {"rm": v["rm"], "ps": v["rm"], "fp8": v["fp8"]}
                          for k, v in ops.DECODE_WAVES.items()})
+    monkeypatch.setattr(ops, "DECODE_WAVES_MT2", {})
     torch.manual_seed(21)
     dt, H, bs = torch.bfloat16, 1024, 16
     x = torch.randn(m, H, dtype=dt, device="cuda")
@@ -757,11 +758,12 @@ def test_fp8_decode_kernels_vs_fp32_reference(m):
     close(vc, vc_r, 3e-2, 3e-2)
 
 
-@pytest.mark.parametrize("m", [1, 5, 16])
+@pytest.mark.parametrize("m", [1, 5, 16, 17, 32])
 def test_decode_gate_up_silu_8b_shape(m):
     """gate_up + SiLU at the Llama-3.1-8B decode shape (inter 14336, K 4096, pre-shuffled):
     1792 tiles - a multiple of the CU count, so with ATTA_GU_PERSIST=1 this runs the
-    persistent one-pipeline-per-CU variant (gemv.hip silu_persist_kernel) - vs fp32."""
+    persistent one-pipeline-per-CU variant (gemv.hip silu_persist_kernel) - vs fp32.
+    m 17 / 32: two MFMA row blocks at ops.DECODE_WAVES_MT2's wave count (small-prefill path)."""
     torch.manual_seed(m)
     dt = torch.bfloat16
     inter, H = 14336, 4096
