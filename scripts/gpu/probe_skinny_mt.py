@@ -42,13 +42,48 @@ def sweep_linear():
             print(f"{proj:5s} M={m:3d}: " + "  ".join(row), flush=True)
 
 
+def time_qkv_rope():
+    """fused RMSNorm + QKV + RoPE + KV write (8B shapes, pre-shuffled) at 16 / 17 / 32 rows;
+    the wave count comes from ops.decode_waves (ATTA_DECODE_WAVES=qkv.ps=N to sweep)."""
+    n, k, hq, hkv, bs, nb = 6144, 4096, 32, 8, 16, 64
+    ws = [ops.preshuffle((torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16), "qkv")
+          for _ in range(4)]
+    kc = torch.zeros(nb, hkv, bs, 128, dtype=torch.bfloat16, device="cuda")
+    vc = torch.zeros(nb, hkv, 128, bs, dtype=torch.bfloat16, device="cuda")
+    cs = ops.ref.rope_cos_sin(128, 4096, 500000.0, None, device="cuda")
+    for m in (16, 17, 32):
+        x = torch.randn(m, k, device="cuda").to(torch.bfloat16)
+        pos = torch.arange(m, dtype=torch.int32, device="cuda")
+        slots = torch.arange(m, dtype=torch.int32, device="cuda")
+        q = torch.empty(m, hq, 128, dtype=torch.bfloat16, device="cuda")
+
+        def run(i):
+            ops.decode_qkv_rope(x, ws[i % 4], 1e-5, pos, slots, cs, kc, vc, hq, hkv, q_out=q,
+                                preshuffled=True)
+        for i in range(3):
+            run(i)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(40):
+            run(i)
+        e1.record()
+        torch.cuda.synchronize()
+        print(f"qkv_rope waves={ops.decode_waves('qkv', True)} M={m:3d}: "
+              f"{e0.elapsed_time(e1) * 1e3 / 40:6.1f} us", flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only-m", type=int, default=0)
     ap.add_argument("--sweep-linear", action="store_true")
+    ap.add_argument("--qkv-rope", action="store_true")
     a = ap.parse_args()
     if a.sweep_linear:
         sweep_linear()
+        return
+    if a.qkv_rope:
+        time_qkv_rope()
         return
     n, k = 28672, 4096
     copies = 4
