@@ -760,10 +760,8 @@ def test_fp8_decode_kernels_vs_fp32_reference(m):
 
 @pytest.mark.parametrize("m", [1, 5, 16, 17, 32])
 def test_decode_gate_up_silu_8b_shape(m):
-    """gate_up + SiLU at the Llama-3.1-8B decode shape (inter 14336, K 4096, pre-shuffled):
-    1792 tiles - a multiple of the CU count, so with ATTA_GU_PERSIST=1 this runs the
-    persistent one-pipeline-per-CU variant (gemv.hip silu_persist_kernel) - vs fp32.
-    m 17 / 32: two MFMA row blocks at ops.DECODE_WAVES_MT2's wave count (small-prefill path)."""
+    """gate_up + SiLU at the Llama-3.1-8B decode shape (inter 14336, K 4096, pre-shuffled,
+    1792 16-row tiles) vs fp32.  m 17 / 32: two MFMA row blocks at ops.DECODE_WAVES_MT2's wave count (small-prefill path)."""
     torch.manual_seed(m)
     dt = torch.bfloat16
     inter, H = 14336, 4096
