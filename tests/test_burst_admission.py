@@ -74,9 +74,11 @@ def test_burst_window_zero_disables_holding():
 
 def test_straggler_after_deadline_not_held_again():
     """A sibling arriving after its burst was flushed at the deadline is admitted at once."""
-    plan = [(0.0, "e0", ("task-5", 2)), (0.3, "e1", ("task-5", 2))]
-    steps, ttft, ae = _run(0.05, plan)
-    assert ttft["e1"] < 0.04, ttft  # no second 50 ms window
+    # a 250 ms window keeps "held again" (>= 0.25 s) far from a loaded CPU's step time
+    plan = [(0.0, "e0", ("task-5", 2)), (0.6, "e1", ("task-5", 2))]
+    steps, ttft, ae = _run(0.25, plan)
+    assert ttft["e0"] >= 0.2, ttft  # the first one was held for the window
+    assert ttft["e1"] < 0.15, ttft  # no second window
 
 
 # ---- deterministic policy tests on _take_pending (no engine thread, controlled clock) -----
