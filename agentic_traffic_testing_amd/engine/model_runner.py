@@ -193,7 +193,10 @@ class ModelRunner:
         self._tok_done = [torch.cuda.Event() if self.is_cuda else None for _ in range(2)]
         # the prefill GEMM's error word as of the last prefill step (0: every wait succeeded)
         self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=pin)
+        # OR of the words read since the last take_kernel_error() (the device word is cleared
+        # on every read), and how many steps ever reported one
         self.kernel_error = 0
+        self.kernel_error_steps = 0
         self._last_collect = 0.0
         nkv = self.model.n_kv_heads
         self.part_out = torch.empty(self.max_seqs * nkv * alloc_parts * 16 * 128,
@@ -220,6 +223,7 @@ class ModelRunner:
         # the fused decode attention combines <= 64 partitions in-kernel (<= 16k tokens at
         # 256-token partitions); longer contexts use the two-kernel split-K path
         self.fused_decode = bool(cfg.fused_decode) and self.max_parts <= 64
+        self.model.fused_decode = self.fused_decode
         # keyed (batch bucket, partition bucket)
         self.graphs: dict[tuple, torch.cuda.CUDAGraph] = {}
         self.graph_io: dict[tuple, dict] = {}
@@ -278,7 +282,8 @@ class ModelRunner:
         self.num_blocks = nb
         shape_k = (L, nb, m.n_kv_heads, self.block_size, m.head_dim)
         shape_v = (L, nb, m.n_kv_heads, m.head_dim, self.block_size)
-        # zero-init: pages read past a sequence's end must hold finite values
+        # zero-init (tidy, not required: the attention kernels zero the V of every key past a
+        # sequence's end before P.V, so stale or non-finite bytes there are harmless)
         self.k_cache = torch.zeros(shape_k, dtype=self.dtype, device=self.device)
         self.v_cache = torch.zeros(shape_v, dtype=self.dtype, device=self.device)
         self.k_layers = [self.k_cache[i] for i in range(L)]
@@ -309,7 +314,7 @@ class ModelRunner:
             # steps the fused small-prefill path takes (<= SKINNY_MAX_M rows) stay unpadded:
             # its GEMVs read every row of x per weight tile (17 rows padded to 32 doubled
             # gate_up: 80 vs ~40 us)
-            if not (self.model.small_prefill_fused and rows <= ops.SKINNY_MAX_M):
+            if not self.model.small_prefill_ok(rows):
                 pad_tokens = bucket_rows(rows)
         d = self.bm.build_batch(ids, qs, ql, self.bt_width,
                                 self.tile_tokens if tiles else 0, batch.num_decode, pad_tokens,
@@ -474,14 +479,23 @@ class ModelRunner:
             # prefill rows ran: fetch the hand-written GEMM's error word with the tokens'
             # own sync (a cross-workgroup wait that timed out - outputs are still exact, the
             # workgroup recomputed; it signals a GPU shared with other work) - ADVICE r3
-            ops.prefill_gemm_error_to(self._err_host)
+            self._err_host.zero_()
+            ops.prefill_gemm_error_to(self._err_host, clear=True)
         out = toks[:n].cpu().numpy()
-        if self.is_cuda and int(self._err_host[0]) != self.kernel_error:
-            self.kernel_error = int(self._err_host[0])
-            print(f"[model_runner] prefill GEMM error word {self.kernel_error:#x}: a "
+        word = int(self._err_host[0]) if self.is_cuda else 0
+        if word:
+            self._err_host.zero_()
+            self.kernel_error |= word
+            self.kernel_error_steps += 1
+            print(f"[model_runner] prefill GEMM error word {word:#x}: a "
                   "cross-workgroup wait timed out (tiles recomputed, outputs exact; the GPU "
                   "is shared or oversubscribed)", flush=True)
         return out
+
+    def take_kernel_error(self) -> int:
+        """Error words seen since the previous call (the /health check), then cleared."""
+        w, self.kernel_error = self.kernel_error, 0
+        return w
 
     def launchable(self, batch: Batch) -> bool:
         """Decode-only batches can be launched asynchronously (every sampler runs on the

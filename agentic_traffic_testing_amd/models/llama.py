@@ -90,6 +90,9 @@ class LlamaModel:
         self.prefill_gemm_min_rows = 128
         # prefill steps of <= 32 rows on the fused decode kernels (EngineConfig.small_prefill_fused)
         self.small_prefill_fused = True
+        # the runner's fused-decode switch (EngineConfig.fused_decode): off also turns the
+        # fused kernels off for small prefill steps
+        self.fused_decode = True
         self.cfg = cfg
         self.dtype = dtype
         self.device = torch.device(device)
@@ -190,12 +193,18 @@ class LlamaModel:
         gu = (gu.float() * n_post.float()[None, :]).to(gu.dtype).contiguous()
         ones = self._ones(n_in)
         if self.quant == "fp8":
-            return self._quantize_layer(ones, qkv, o, gu, down)
+            # row-parallel shards (o, down: a K slice of every row) quantise with the FULL
+            # row's scale, so TP=N fp8 weights equal TP=1's bit for bit
+            full = self.tp_size > 1
+            amax = (wo.float().abs().amax(1) if full else None,
+                    wd.float().abs().amax(1) if full else None)
+            return self._quantize_layer(ones, qkv, o, gu, down, amax)
         return LayerWeights(ones, qkv, o, ones, gu, down)
 
-    def _quantize_layer(self, ones, qkv, o, gu, down) -> LayerWeights:
+    def _quantize_layer(self, ones, qkv, o, gu, down, amax=(None, None)) -> LayerWeights:
         """fp8 weight-only quantisation of the four projections (after norm folding)."""
-        qs = [ops.quantize_fp8(w) for w in (qkv, o, gu, down)]
+        qs = [ops.quantize_fp8(qkv), ops.quantize_fp8(o, amax[0]), ops.quantize_fp8(gu),
+              ops.quantize_fp8(down, amax[1])]
         if self.device.type != "cuda":  # CPU reference: the values fp8 can represent
             deq = [ops.dequantize_fp8(q, sc, self.dtype) for q, sc in qs]
             return LayerWeights(ones, deq[0], deq[1], ones, deq[2], deq[3])
@@ -324,8 +333,7 @@ class LlamaModel:
         # attention: 5 launches per layer at weight-stream speed instead of ~9 with the
         # row-major skinny / library GEMMs (17 rows: 168 -> ~80 us of GEMMs per layer,
         # profiles/r4_small_prefill_fused.txt)
-        small = (self.small_prefill_fused and self.device.type == "cuda" and self.tp_size == 1
-                 and not fp8 and T <= ops.SKINNY_MAX_M and self.decode_fusable(T))
+        small = self.small_prefill_ok(T)
         for li, L in enumerate(self.layers):
             ps = L.qkv_ps is not None
             if small:
@@ -458,6 +466,15 @@ class LlamaModel:
             # residual += sum over ranks, the add fused into the IPC reduction's epilogue
             return self.tp_group.all_reduce_residual(self._proj(x, w, scale), residual)
         return self._proj(x, w, scale, residual=residual)
+
+    def small_prefill_ok(self, T: int) -> bool:
+        """Does a (prefill or mixed) step of T rows run on the fused decode kernels - RMSNorm
+        folded into the pre-shuffled skinny GEMVs, RoPE + KV write in the QKV epilogue, SiLU-mul
+        in gate_up?  The one predicate for forward() and the runner's row padding (ADVICE r4:
+        TP / fp8 steps of <= 32 rows take the library path and must be padded to its tuned
+        buckets; fused_decode=False turns the fused kernels off here too)."""
+        return (self.small_prefill_fused and self.fused_decode and self.device.type == "cuda"
+                and self.tp_size == 1 and self.quant != "fp8" and self.decode_fusable(T))
 
     def decode_fusable(self, num_tokens: int) -> bool:
         # 16-bit GEMVs: K % 128 (4 waves x 32); fp8 GEMVs: K % 256 (4 waves x 64)

@@ -419,10 +419,16 @@ def preshuffle(w: torch.Tensor, rowmap: str = "plain") -> torch.Tensor:
 FP8_MAX = 448.0
 
 
-def quantize_fp8(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
-    """[N, K] 16-bit weight -> (uint8 e4m3fn bytes [N, K], fp32 per-row scale [N])."""
+def quantize_fp8(w: torch.Tensor, row_amax: torch.Tensor | None = None
+                 ) -> tuple[torch.Tensor, torch.Tensor]:
+    """[N, K] 16-bit weight -> (uint8 e4m3fn bytes [N, K], fp32 per-row scale [N]).
+
+    ``row_amax`` overrides the per-row |max| the scale is derived from: a TP row-parallel
+    shard (o / down, a K slice of every row) passes the FULL row's amax, so every rank
+    quantises with the TP=1 scale and TP=N fp8 weights are bit-identical to TP=1's."""
     wf = w.float()
-    scale = (wf.abs().amax(dim=1) / FP8_MAX).clamp_min(1e-12)
+    amax = wf.abs().amax(dim=1) if row_amax is None else row_amax.float().to(wf.device)
+    scale = (amax / FP8_MAX).clamp_min(1e-12)
     q = (wf / scale[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
     return q.view(torch.uint8), scale.contiguous()
 
@@ -607,10 +613,16 @@ def prefill_gemm_error() -> int:
     return int(_native().prefill_gemm_error())
 
 
-def prefill_gemm_error_to(host: torch.Tensor) -> None:
+def prefill_gemm_error_to(host: torch.Tensor, clear: bool = True) -> None:
     """Enqueue a copy of the prefill GEMM's error word into ``host`` (pinned int32) on the
-    current stream; read it after the next synchronisation (no extra sync of its own)."""
-    _native().prefill_gemm_error_to(host)
+    current stream; read it after the next synchronisation (no extra sync of its own).
+    ``clear``: zero the word behind the copy, so each read covers the calls since the last."""
+    _native().prefill_gemm_error_to(host, bool(clear))
+
+
+def prefill_gemm_error_reset() -> None:
+    """Zero the prefill GEMM's error word."""
+    _native().prefill_gemm_error_reset()
 
 
 def _need_cuda(x, preshuffled):

@@ -205,6 +205,16 @@ __global__ __launch_bounds__(256) void paged_attention_kernel(AttnParams p) {
     i16x4 pf;
 #pragma unroll
     for (int i = 0; i < 4; ++i) pf[i] = static_cast<short>(from_f32<T>(pv[i]));
+    // V of keys past the sequence end (stale tail slots of the last page) is zeroed: P = 0
+    // there, and 0 * V must not become NaN on a non-finite stale value
+    if (tv + 4 > kvlen) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (tv + i >= kvlen) {
+#pragma unroll
+          for (int dt = 0; dt < 8; ++dt) vf[dt][i] = 0;
+        }
+    }
 
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) {

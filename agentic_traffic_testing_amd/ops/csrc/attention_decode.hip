@@ -183,10 +183,24 @@ __device__ __forceinline__ void decode_attention_body(const DecParams& p, const 
     psum += __shfl_xor(psum, 32, kWave);
     l_run = l_run * alpha + psum;
     m_run = m_new;
+    // keys past the sequence end (the tail slots of its last page) hold stale bytes of the
+    // page's previous owner: P is 0 there, and V is zeroed too so a non-finite stale value
+    // cannot make 0 * V a NaN (wave-uniform edge test: the last tile only)
+    i16x4 vv[8];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) vv[dt] = ft.v[dt];
+    if (kbase + 16 > kend) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (kbase + 4 * grp + j >= kend) {
+#pragma unroll
+          for (int dt = 0; dt < 8; ++dt) vv[dt][j] = 0;
+        }
+    }
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) {
       o[dt] *= alpha;
-      o[dt] = Mf<T>::pv(ft.v[dt], pf, o[dt]);
+      o[dt] = Mf<T>::pv(vv[dt], pf, o[dt]);
     }
   }
   tr[1] = wall_clock64();

@@ -353,11 +353,15 @@ void prefill_gemm(at::Tensor c, const at::Tensor& a, const at::Tensor& w,
 }
 
 int64_t prefill_gemm_error() { return atta_prefill_gemm_error(); }
-void prefill_gemm_error_to(at::Tensor host) {
+void prefill_gemm_error_to(at::Tensor host, bool clear) {
   TORCH_CHECK(host.device().is_cpu() && host.is_pinned() && host.scalar_type() == at::kInt &&
                   host.numel() >= 1,
               "prefill_gemm_error_to: a pinned int32 host tensor");
-  check_rc(atta_prefill_gemm_error_async(host.data_ptr(), cur_stream()), "prefill_gemm_error_to");
+  check_rc(atta_prefill_gemm_error_async(host.data_ptr(), cur_stream(), clear ? 1 : 0),
+           "prefill_gemm_error_to");
+}
+void prefill_gemm_error_reset() {
+  check_rc(atta_prefill_gemm_error_reset(), "prefill_gemm_error_reset");
 }
 int64_t prefill_gemm_auto_bm(int64_t m) { return atta_prefill_gemm_auto_bm(static_cast<int>(m)); }
 void prefill_gemm_config(int64_t schedule, int64_t group_m, int64_t ablate) {
@@ -809,7 +813,8 @@ TORCH_LIBRARY(atta, m) {
   m.def("prefill_gemm(Tensor(a!) c, Tensor a, Tensor w, Tensor? residual, int mode, Tensor? xs=None, Tensor? ws=None, int schedule=-1, int bm=0) -> ()");
   m.def("prefill_gemm_auto_bm(int m) -> int", &prefill_gemm_auto_bm);
   m.def("prefill_gemm_error() -> int", &prefill_gemm_error);
-  m.def("prefill_gemm_error_to(Tensor(a!) host) -> ()", &prefill_gemm_error_to);
+  m.def("prefill_gemm_error_to(Tensor(a!) host, bool clear) -> ()", &prefill_gemm_error_to);
+  m.def("prefill_gemm_error_reset() -> ()", &prefill_gemm_error_reset);
   m.def("prefill_gemm_config(int schedule, int group_m, int ablate=0) -> ()", &prefill_gemm_config);
   m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rms_norm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");

@@ -187,9 +187,11 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
   const int v_lds = (lane >> 1) * kVStride + 16 * wid + 4 * (lane & 1);  // permuted: see kVStride
   // LDS only (the launcher rejects bt_stride > kBtLds): a select between the LDS copy and the
   // global table compiled to FLAT loads, whose vmcnt wait put a dependent global round trip
-  // in front of every block's K/V loads.  Keys past the causal range read a clamped (valid,
-  // finite: the cache is zero-initialised and only ever holds real tokens) page; their
-  // scores are masked and their P is 0.
+  // in front of every block's K/V loads.  Keys past the workgroup's range (>= wg_end) read a
+  // clamped page or the unused tail slots of the last page - stale bytes of whatever sequence
+  // held that page before.  Their scores are masked (P = 0), and their V^T columns are zeroed
+  // at staging (store_block), so a non-finite stale value cannot turn 0 * V into NaN
+  // (no invariant on the cache contents is needed).
   u32x4 kr[kChunks], vr[kChunks];
   auto load_block = [&](int kb) {
     const int pi = min((kb * kKB + 16 * wid) >> p.bs_shift, last_page);
@@ -204,10 +206,23 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
     for (int u = 0; u < kChunks; ++u)
       vr[u] = *reinterpret_cast<const u32x4*>(vb_ + v_lane + u * 32 * BS);
   };
-  auto store_block = [&](int buf) {
+  auto store_block = [&](int buf, int kb) {
 #pragma unroll
     for (int u = 0; u < kChunks; ++u)
       *reinterpret_cast<u32x4*>(&lds_k[buf][k_lds + u * 4 * kKStride]) = kr[u];
+    // this lane's 8 V keys: kb * kKB + 16 wid + 8 (lane & 1) + j; only the last block can
+    // reach past wg_end (uniform per workgroup except at that edge)
+    const int vkey = kb * kKB + 16 * wid + 8 * (lane & 1);
+    if (vkey + 8 > wg_end) {
+#pragma unroll
+      for (int u = 0; u < kChunks; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const unsigned lo = vkey + 2 * j < wg_end ? 0x0000ffffu : 0u;
+          const unsigned hi = vkey + 2 * j + 1 < wg_end ? 0xffff0000u : 0u;
+          vr[u][j] &= (lo | hi);
+        }
+    }
 #pragma unroll
     for (int u = 0; u < kChunks; ++u) {
       // keys 8 g .. 8 g + 3 -> columns 4 g .., keys 8 g + 4 .. 8 g + 7 -> columns 8 + 4 g ..
@@ -226,7 +241,7 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
 
   if (nblocks > 0) {
     load_block(0);
-    store_block(0);
+    store_block(0, 0);
   }
   __syncthreads();
 
@@ -337,7 +352,7 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
       }
     }
     if (more && !issued) load_block(kb + 1);  // waves with no visible key in this block
-    if (more) store_block(buf ^ 1);
+    if (more) store_block(buf ^ 1, kb + 1);
     __syncthreads();
   }
 

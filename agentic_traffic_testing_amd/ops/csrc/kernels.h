@@ -147,5 +147,6 @@ int atta_prefill_gemm(void* c, const void* a, const void* w, const void* res, in
                       hipStream_t stream);
 int atta_prefill_gemm_auto_bm(int M);
 int atta_prefill_gemm_error();
-int atta_prefill_gemm_error_async(void* host, hipStream_t stream);
+int atta_prefill_gemm_error_async(void* host, hipStream_t stream, int clear);
+int atta_prefill_gemm_error_reset();
 int atta_prefill_gemm_config(int schedule, int group_m, int ablate);

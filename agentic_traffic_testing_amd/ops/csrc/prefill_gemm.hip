@@ -842,13 +842,25 @@ int atta_prefill_gemm_error() {
 
 // Enqueue a copy of the error word into `host` (4 bytes, pinned) on `stream`: the engine reads
 // it after the step's own token sync, so the check costs no extra synchronisation.
-int atta_prefill_gemm_error_async(void* host, hipStream_t stream) {
+// clear != 0: the word is zeroed behind the copy (stream order), so every read reports the
+// timeouts since the previous read, not "ever" (ADVICE r4).
+int atta_prefill_gemm_error_async(void* host, hipStream_t stream, int clear) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return -2;
   Workspace* s = workspace(dev);
   if (s == nullptr) return -2;
-  return hipMemcpyAsync(host, s->err, sizeof(unsigned), hipMemcpyDeviceToHost, stream) ==
-                 hipSuccess
-             ? 0
-             : -2;
+  if (hipMemcpyAsync(host, s->err, sizeof(unsigned), hipMemcpyDeviceToHost, stream) !=
+      hipSuccess)
+    return -2;
+  if (clear && hipMemsetAsync(s->err, 0, sizeof(unsigned), stream) != hipSuccess) return -2;
+  return 0;
+}
+
+// Zero the error word (tests that force a timeout re-arm it in their finally block).
+int atta_prefill_gemm_error_reset() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -2;
+  Workspace* s = workspace(dev);
+  if (s == nullptr) return 0;  // no workspace yet: nothing recorded
+  return hipMemset(s->err, 0, sizeof(unsigned)) == hipSuccess ? 0 : -2;
 }

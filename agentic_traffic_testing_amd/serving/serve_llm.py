@@ -150,10 +150,13 @@ async def handle_health(request: web.Request) -> web.Response:
                                  status=503)
     # kernel error word (prefill GEMM wait timed out -> tiles recomputed, outputs exact): the
     # GPU is shared or oversubscribed; still serving, so 200 with the reason attached
-    err = getattr(getattr(st.engine, "runner", None), "kernel_error", 0) if st.engine else 0
+    # (words since the previous /health check: the runner clears them on read)
+    runner = getattr(st.engine, "runner", None) if st.engine else None
+    err = runner.take_kernel_error() if hasattr(runner, "take_kernel_error") else 0
     if err:
         return web.json_response({"status": "ok", "degraded": True,
-                                  "kernel_error_word": int(err)})
+                                  "kernel_error_word": int(err),
+                                  "kernel_error_steps": int(runner.kernel_error_steps)})
     return web.json_response({"status": "ok"})
 
 

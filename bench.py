@@ -47,6 +47,24 @@ DATA = ("synthetic (agent fan-out prompts, synthetic tokenizer, seeded random-in
         "weights)")
 
 
+def metric_name(label: str, tp: int = 1, quantization: str = "") -> str:
+    """The metric string of one run: BASELINE.json's exact METRIC for the headline model at
+    TP=1 (a DP replica is a TP=1 engine), otherwise the same template naming the model that
+    actually ran, its TP degree and fp8 weights - so a 70B TP=8 record never calls itself
+    'Llama-3-8B TP=1'."""
+    low = label.lower()
+    if "70b" in low:
+        fam = "Llama-3-70B"
+    elif "8b" in low:
+        fam = "Llama-3-8B"
+    else:
+        fam = label
+    if fam == "Llama-3-8B" and tp == 1 and not quantization:
+        return METRIC
+    q = f" {quantization}" if quantization else ""
+    return f"llm-backend tokens/sec + p50 TTFT under 5-agent fan-out, {fam} TP={tp}{q}"
+
+
 def overrides(items: list[str]) -> dict:
     """--set key=value pairs -> EngineConfig kwargs, typed like the field's default."""
     from dataclasses import fields
@@ -231,6 +249,14 @@ def main_dp(a, world: int):
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     _window_marker(a)
+    # One untimed COLD episode after the timed region: prefix cache dropped first, so every
+    # prompt row is prefilled.  The timed episodes cycle 4 tasks and hit the prefix cache from
+    # episode 5 on (only the "(episode N)" suffix is new), so their TTFT is the cached regime;
+    # this line reports the uncached one beside it.  Not part of value / ms_per_step.
+    cold = None
+    if a.steps > 0:
+        eng.runner.reset_state()
+        cold = wl.run_episode()
 
     if a.verbose and rank == 0:
         tm = eng.timing
@@ -243,22 +269,15 @@ def main_dp(a, world: int):
             f"replay+sync {rt['graph_run'] / g * 1e3:.3f} ms")
     tokens = sum(r.completion_tokens for r in results)
     ttfts = [t for r in results for t in r.ttfts]
-    # TTFT by phase of the episode: rows actually prefilled (prompt - prefix-cache hits) and
-    # the median TTFT of the phase's requests
-    by_phase = {}
-    for r in results:
-        for name, pt, ct, tt in r.phases:
-            d = by_phase.setdefault(name, {"rows": [], "ttft": []})
-            d["rows"].append(pt - ct)
-            d["ttft"].extend(tt)
-    ttft_phases = {k: {"prefill_rows": int(statistics.median(v["rows"])),
-                       "p50_ttft_ms": round(statistics.median(v["ttft"]) * 1e3, 2)}
-                   for k, v in by_phase.items()}
+    ttft_phases = _phase_table(results)
+    cold_phases = _phase_table([cold]) if cold is not None else {}
+    cold_ttfts = list(cold.ttfts) if cold is not None else []
     lat = [t for r in results for t in r.latencies]
     per_rank = [round(tokens / elapsed, 2)]
     if dist:
         gathered = [None] * world
-        dist.all_gather_object(gathered, (elapsed, tokens, ttfts, lat))
+        dist.all_gather_object(gathered, (elapsed, tokens, ttfts, lat, cold_ttfts))
+        cold_ttfts = [t for g in gathered for t in g[4]]
         elapsed = max(g[0] for g in gathered)
         tokens = sum(g[1] for g in gathered)
         per_rank = [round(g[1] / g[0], 2) for g in gathered]
@@ -272,7 +291,7 @@ def main_dp(a, world: int):
         p95 = srt[min(len(srt) - 1, int(0.95 * len(srt)))] if srt else None
         label = _model_label(a)
         out = {
-            "metric": METRIC,
+            "metric": metric_name(label, 1, a.quantization),
             "value": round(value, 2),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -303,6 +322,9 @@ def main_dp(a, world: int):
             "p95_ttft_s": round(p95, 4) if p95 is not None else None,
             "p50_latency_s": round(statistics.median(lat), 3) if lat else None,
             "ttft_by_phase": ttft_phases,
+            "p50_ttft_uncached_s": (round(statistics.median(cold_ttfts), 4)
+                                    if cold_ttfts else None),
+            "ttft_by_phase_uncached": cold_phases,
             "requests_per_step_per_gpu": 2 + a.fanout,
             "completion_tokens": int(tokens),
             "init_s": round(init_s, 1),
@@ -312,6 +334,20 @@ def main_dp(a, world: int):
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def _phase_table(results) -> dict:
+    """TTFT by phase of the episode: rows actually prefilled (prompt - prefix-cache hits) and
+    the median TTFT of the phase's requests."""
+    by_phase = {}
+    for r in results:
+        for name, pt, ct, tt in r.phases:
+            d = by_phase.setdefault(name, {"rows": [], "ttft": []})
+            d["rows"].append(pt - ct)
+            d["ttft"].extend(tt)
+    return {k: {"prefill_rows": int(statistics.median(v["rows"])),
+                "p50_ttft_ms": round(statistics.median(v["ttft"]) * 1e3, 2)}
+            for k, v in by_phase.items()}
 
 
 def _finish_http(a, eng, world, rank, dist, init_s, cfg, log):
@@ -339,8 +375,8 @@ def _finish_http(a, eng, world, rank, dist, init_s, cfg, log):
     if rank == 0:
         label = _model_label(a)
         print(json.dumps({
-            "metric": METRIC, "value": round(tokens / elapsed, 2), "unit": "tokens/s",
-            "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "metric": metric_name(label, 1, a.quantization), "value": round(tokens / elapsed, 2),
+            "unit": "tokens/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1000.0, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16" if "bf" in a.dtype else a.dtype,
@@ -402,8 +438,8 @@ def main_tp(a):
     ttfts = sorted(t for r in results for t in r.ttfts)
     label = _model_label(a)
     out = {
-        "metric": METRIC, "value": round(tokens / elapsed, 2), "unit": "tokens/s",
-        "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "metric": metric_name(label, world, a.quantization), "value": round(tokens / elapsed, 2),
+        "unit": "tokens/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1000.0, 2), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "bf16" if "bf" in a.dtype else a.dtype,
         "weights": a.quantization or ("bf16" if "bf" in a.dtype else a.dtype),

@@ -7,7 +7,7 @@ from agentic_traffic_testing_amd.config import EngineConfig
 from agentic_traffic_testing_amd.engine.llm_engine import LLMEngine
 from agentic_traffic_testing_amd.engine.sequence import SamplingParams
 
-from helpers import dense_logits, greedy_reference
+from helpers import dense_logits
 
 
 def _prompts(seed=0, vocab=3000):
@@ -18,25 +18,33 @@ def _prompts(seed=0, vocab=3000):
 
 
 def _check(eng, prompts, n=6, tol_logit=None):
+    """Teacher-forced greedy check of EVERY generated position: the dense
+    oracle runs on the engine's own prefix (prompt + the engine's tokens so far), so a near-tie
+    flip does not hide the positions after it.  Every position where the engine's token is not
+    the oracle's argmax must be a near tie (< tol_logit), and at most one position in five may
+    diverge at all (a drifting path flips most of them).  Returns (outputs, divergent
+    sequences)."""
     sp = SamplingParams(temperature=0.0, max_tokens=n, ignore_eos=True)
     outs = eng.generate(prompts, sp)
     assert len(outs) == len(prompts)
     m = eng.runner.model
-    bad = 0
+    bad_seqs = bad_pos = checked = 0
     for p, o in zip(prompts, outs):
-        exp = greedy_reference(m, p, n)
-        if o.token_ids != exp:
-            # allow divergence only where the oracle's top-2 logits are a near tie
-            ids = list(p)
-            for got_t, exp_t in zip(o.token_ids, exp):
-                if got_t != exp_t:
-                    lg = dense_logits(m, ids)
-                    top = torch.topk(lg, 2).values
-                    assert float(top[0] - lg[got_t]) < (tol_logit or 0.05), (o.token_ids, exp)
-                    bad += 1
-                    break
-                ids.append(got_t)
-    return outs, bad
+        assert len(o.token_ids) == n
+        ids = list(p)
+        diverged = False
+        for got_t in o.token_ids:
+            lg = dense_logits(m, ids)
+            checked += 1
+            if int(torch.argmax(lg)) != got_t:
+                gap = float(lg.max() - lg[got_t])
+                assert gap < (tol_logit or 0.05), (o.token_ids, len(ids) - len(p), gap)
+                bad_pos += 1
+                diverged = True
+            ids.append(got_t)
+        bad_seqs += diverged
+    assert bad_pos <= max(1, checked // 5), (bad_seqs, bad_pos, checked)
+    return outs, bad_seqs
 
 
 def test_engine_cpu_matches_dense():
@@ -498,3 +506,87 @@ def test_prefill_splitk_route_engine_matches_oracle(model, monkeypatch):
     assert bad <= 1
     assert calls.count("splitk") == eng.runner.model.cfg.num_layers, calls
     assert ops.prefill_gemm_error() == 0
+
+
+
+def _small_prefill_scenario(eng, vocab):
+    """Three step shapes that take the fused small-prefill path (<= 32 rows): a lone 17-token
+    prompt; a prompt that hits the prefix cache with 5 new rows; a step mixing two decoding
+    sequences with a 9-token prefill.  Returns {request id: (prompt, token ids)}."""
+    rng = np.random.default_rng(31)
+    sp = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
+    prompts = {"lone": rng.integers(300, vocab, size=17).tolist(),
+               "base": rng.integers(300, vocab, size=40).tolist()}
+    outs = eng.generate([prompts["lone"], prompts["base"]], sp)
+    res = {k: (prompts[k], o.token_ids) for k, o in zip(("lone", "base"), outs)}
+    # prefix hit: 2 cached blocks (32 tokens) + 5 new rows
+    hit = prompts["base"][:32] + rng.integers(300, vocab, size=5).tolist()
+    o = eng.generate([hit], sp)[0]
+    assert o.cached_prompt_tokens == 32
+    res["hit"] = (hit, o.token_ids)
+    # mixed step: two sequences decoding, then a 9-token prompt joins them
+    mixed = {"d0": rng.integers(300, vocab, size=12).tolist(),
+             "d1": rng.integers(300, vocab, size=7).tolist(),
+             "mix": rng.integers(300, vocab, size=9).tolist()}
+    long_sp = SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True)
+    eng.add_request("d0", mixed["d0"], long_sp)
+    eng.add_request("d1", mixed["d1"], long_sp)
+    done = {}
+    for _ in range(3):
+        for r in eng.step():
+            if r.finished:
+                done[r.request_id] = r.token_ids
+    eng.add_request("mix", mixed["mix"], sp)
+    while len(done) < 3:
+        for r in eng.step():
+            if r.finished:
+                done[r.request_id] = r.token_ids
+    res.update({k: (mixed[k], done[k]) for k in mixed})
+    return res
+
+
+@pytest.mark.gpu
+def test_small_prefill_fused_matches_unfused_and_oracle():
+    """prefill / mixed steps of <= 32 rows run the norm-folded
+    pre-shuffled GEMVs (RoPE + KV write in the QKV epilogue, SiLU in gate_up).  The same
+    scenario with small_prefill_fused on and off (same seeded weights): every request's tokens
+    are checked teacher-forced against the dense oracle (near-tie rule, at most one divergent
+    position in five), the two paths agree on all but one request, and the KV cache pages both
+    wrote agree to bf16 rounding."""
+    vocab = 16000
+    res, caches = {}, {}
+    m = None
+    for fused in (True, False):
+        eng = LLMEngine(EngineConfig(model="llama-8b-slice", device="cuda", max_model_len=512,
+                                     num_kv_blocks=256, max_num_seqs=8,
+                                     max_num_batched_tokens=512, graph_batch_sizes=(1, 2, 4),
+                                     small_prefill_fused=fused))
+        assert eng.runner.model.small_prefill_ok(17) == fused
+        res[fused] = _small_prefill_scenario(eng, vocab)
+        torch.cuda.synchronize()
+        caches[fused] = (eng.runner.k_cache.float().cpu(), eng.runner.v_cache.float().cpu())
+        m = eng.runner.model
+        if fused:
+            del eng
+            torch.cuda.empty_cache()
+    assert res[True].keys() == res[False].keys()
+    bad_pos = checked = 0
+    for fused in (True, False):
+        for rid, (prompt, toks) in res[fused].items():
+            ids = list(prompt)
+            for t in toks:
+                lg = dense_logits(m, ids)
+                checked += 1
+                if int(torch.argmax(lg)) != t:
+                    gap = float(lg.max() - lg[t])
+                    assert gap < 0.25, (fused, rid, len(ids) - len(prompt), gap)
+                    bad_pos += 1
+                ids.append(t)
+    assert bad_pos <= checked // 5, (bad_pos, checked)
+    same = sum(res[True][r][1] == res[False][r][1] for r in res[True])
+    assert same >= len(res[True]) - 1, (res[True], res[False])
+    if same < len(res[True]):
+        return  # a near-tie flip: later KV pages legitimately hold different tokens
+    for a, b in zip(caches[True], caches[False]):
+        tol = 0.03 * float(b.abs().max()) + 1e-3
+        assert float((a - b).abs().max()) <= tol, float((a - b).abs().max())

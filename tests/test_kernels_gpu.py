@@ -522,6 +522,59 @@ def test_attention_decode_v2(hq, hkv, part_tokens):
         assert bool((cnt == 0).all())
 
 
+def _poison_tails(k, v, bt, kvlen, bs, used_pages):
+    """Every cache slot no sequence owns - the tail slots of each sequence's last page and
+    the unused pages - gets Inf / NaN (the kernels must not rely on a finite,
+    zero-initialised cache past a sequence's end)."""
+    kv = kvlen.cpu().tolist()
+    btc = bt.cpu()
+    for i, n in enumerate(kv):
+        if n % bs:
+            pg = int(btc[i, (n - 1) // bs])
+            k[pg, :, n % bs:, :] = float("inf")
+            v[pg, :, :, n % bs:] = float("nan")
+    free = [p for p in range(k.shape[0]) if p not in used_pages]
+    for p in free:
+        k[p] = float("nan")
+        v[p] = float("inf")
+
+
+def test_attention_kernels_ignore_nonfinite_stale_slots():
+    """Inf / NaN in cache slots past every sequence's end: flash and v1 prefill, the
+    two-kernel decode and the in-kernel-combine decode all stay finite and exact."""
+    torch.manual_seed(21)
+    dt, bs, hq, hkv = torch.bfloat16, 16, 32, 8
+    seqs = [(53, 53), (300, 77), (17, 1), (130, 2)]
+    k, v, bt, kvlen, qstart, T = _make_paged(seqs, hkv, bs, dt)
+    used = {int(bt[i, j]) for i, (kv, _) in enumerate(seqs) for j in range(math.ceil(kv / bs))}
+    q = torch.randn(T, hq, 128, dtype=dt, device="cuda")
+    scale = 1 / math.sqrt(128)
+    exp = ref.paged_attention(q, k, v, bt.clamp(min=0), kvlen, qstart, scale)
+    _poison_tails(k, v, bt, kvlen, bs, used)
+    bt0 = bt.clamp(min=0)  # page 0 is a real page here: its tail may be poisoned too
+    for impl in ("flash", "v1"):
+        ts, to = _tiles(seqs, ops.prefill_tile_tokens(hq // hkv, impl))
+        got = ops.attention_prefill(q, k, v, bt0, kvlen, qstart, ts, to, scale, impl=impl)
+        assert bool(torch.isfinite(got).all()), impl
+        close(got, exp, 1.5e-2, 2e-2)
+    # decode: one query row per sequence (the last prompt token)
+    dseqs = [(kv, 1) for kv, _ in seqs]
+    qd = torch.stack([q[int(qstart[i + 1]) - 1] for i in range(len(seqs))])
+    qs_d = torch.arange(len(seqs) + 1, dtype=torch.int32, device="cuda")
+    exp_d = torch.stack([exp[int(qstart[i + 1]) - 1] for i in range(len(seqs))])
+    S = len(dseqs)
+    po = torch.empty(S * hkv * 8 * 16 * 128, device="cuda")
+    pl = torch.empty(S * hkv * 8 * 16, device="cuda")
+    got = ops.attention_decode(qd, k, v, bt0, kvlen, qs_d, scale, po, pl, 4, 128)
+    assert bool(torch.isfinite(got).all())
+    close(got, exp_d, 1.5e-2, 2e-2)
+    cnt = torch.zeros(S * hkv, dtype=torch.int32, device="cuda")
+    out = torch.empty_like(qd)
+    ops.attention_decode_v2(qd, k, v, bt0, kvlen, qs_d, scale, po, pl, cnt, 8, 128, out=out)
+    assert bool(torch.isfinite(out).all())
+    close(out, exp_d, 1.5e-2, 2e-2)
+
+
 def test_attention_decode_v2_grid_invariant():
     """The partition grid (decode graphs are captured per partition bucket) must not change a
     single bit: a grid of exactly the partitions needed, one more, and max_model_len's."""

@@ -226,12 +226,17 @@ def test_prefill_gemm_timed_out_wait_recomputes(sched, mode):
         torch.cuda.synchronize()
     finally:
         ops.prefill_gemm_config("hybrid")
-    _check(got, exp, K)
-    assert ops.prefill_gemm_error() & 4
-    # the protocol state is re-armed: a normal call afterwards is exact and times out nowhere
-    got2 = ops.prefill_gemm(x, w, mode, schedule=sched, bm=128)
-    torch.cuda.synchronize()
-    _check(got2, exp, K)
+    try:
+        _check(got, exp, K)
+        assert ops.prefill_gemm_error() & 4
+        # the protocol state is re-armed: a normal call afterwards is exact
+        ops.prefill_gemm_error_reset()
+        got2 = ops.prefill_gemm(x, w, mode, schedule=sched, bm=128)
+        torch.cuda.synchronize()
+        _check(got2, exp, K)
+        assert ops.prefill_gemm_error() == 0  # and times out nowhere
+    finally:
+        ops.prefill_gemm_error_reset()  # later tests assert a clean word
 
 
 def test_prefill_gemm_per_call_schedule_keeps_process_config(monkeypatch):
