@@ -116,6 +116,14 @@ MODEL_PRESETS: dict[str, ModelConfig] = {
                                       num_heads=64, num_kv_heads=8, rope_scaling=None,
                                       max_position_embeddings=16384, bos_token_id=16000,
                                       eos_token_ids=(16001, 16009)),
+    # the same per-rank geometry for fp8 weights (BASELINE config 5): the fp8 GEMVs stream K in
+    # 256-wide steps (4 waves x 64), so the FFN shard must be a multiple of 256 at TP=8 - the
+    # real 70B's 28672 / 8 = 3584 is; this slice's 14336 / 8 = 1792 = 7 x 256 is too
+    "llama-70b-tp-slice-fp8": ModelConfig(name="llama-70b-tp-slice-fp8", vocab_size=16384,
+                                          hidden_size=8192, intermediate_size=14336,
+                                          num_layers=2, num_heads=64, num_kv_heads=8,
+                                          rope_scaling=None, max_position_embeddings=16384,
+                                          bos_token_id=16000, eos_token_ids=(16001, 16009)),
     "llama-70b-slice": ModelConfig(name="llama-70b-slice", vocab_size=16384, hidden_size=8192,
                                    intermediate_size=3584, num_layers=2, num_heads=64,
                                    num_kv_heads=8, rope_scaling=None,

@@ -477,11 +477,21 @@ class LlamaModel:
                 and self.tp_size == 1 and self.quant != "fp8" and self.decode_fusable(T))
 
     def decode_fusable(self, num_tokens: int) -> bool:
+        """Can a step of this many rows run the fused weight-streaming kernels?  <= 32 rows:
+        the 16-row-tile GEMVs (any layout); 33..WIDE_MAX_M rows: the wide small-M kernel,
+        which needs the pre-shuffled 16-bit weights (TP=1: the TP decode step's push /
+        one-shot collectives are sized for <= 32 rows)."""
         # 16-bit GEMVs: K % 128 (4 waves x 32); fp8 GEMVs: K % 256 (4 waves x 64)
         step = 256 if self.quant == "fp8" else 128
-        return (self.device.type == "cuda" and num_tokens <= ops.SKINNY_MAX_M
-                and self.cfg.hidden_size % step == 0 and self.inter % step == 0
-                and (self.n_heads * self.head_dim) % step == 0)
+        dims = (self.device.type == "cuda" and self.cfg.hidden_size % step == 0
+                and self.inter % step == 0 and (self.n_heads * self.head_dim) % step == 0)
+        if not dims or num_tokens < 1:
+            return False
+        if num_tokens <= ops.SKINNY_MAX_M:
+            return True
+        return (num_tokens <= ops.WIDE_MAX_M and self.quant != "fp8" and self.tp_size == 1
+                and bool(self.layers) and self.layers[0].qkv_ps is not None
+                and self.lm_head_ps is not None)
 
     def hidden_fusable(self) -> bool:
         """The LM-head GEMV streams K = hidden in 128-wide (16-bit) wave steps."""

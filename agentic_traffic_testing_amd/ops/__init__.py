@@ -309,6 +309,11 @@ def sample(logits, temperature, seeds, steps, out=None):
 # skinny-GEMM (decode) dispatch: rows <= SKINNY_MAX_M use the MFMA weight-streaming kernel,
 # larger M (prefill) goes to hipBLASLt through F.linear.
 SKINNY_MAX_M = int(os.environ.get("ATTA_SKINNY_MAX_M", "32"))
+# 33..WIDE_MAX_M rows over PRE-SHUFFLED 16-bit weights run the wide small-M kernel
+# (csrc/wide.hip: x staged once per workgroup in LDS and shared by its tiles, split-K for the
+# narrow projections), with the same fused epilogues - burst prefills and decode batches of
+# up to 128 sequences.  0 turns it off.
+WIDE_MAX_M = int(os.environ.get("ATTA_WIDE_MAX_M", "128"))
 SKINNY_WAVES = int(os.environ.get("ATTA_SKINNY_WAVES", "8"))
 # per-projection wave counts from the MI355X sweep (profiles/r1_microbench_v3_plain.txt):
 # 8 waves x 2-deep stages for the small qkv / o projections, 16 waves for the large ones.
@@ -393,10 +398,21 @@ def _ksplit(proj: str, x: torch.Tensor, ksplit: int | None, tiles: int) -> int:
     return k
 
 
-def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+def skinny_ok(x: torch.Tensor, w: torch.Tensor, preshuffled: bool = False,
+              fp8: bool = False) -> bool:
+    """Does ``x @ w.T`` run on the MFMA weight-streaming kernels?  <= SKINNY_MAX_M rows on
+    any 16-bit / fp8 layout (gemv.hip); up to WIDE_MAX_M rows on pre-shuffled 16-bit weights
+    (wide.hip)."""
     m, k = x.shape
-    return (x.is_cuda and 1 <= m <= SKINNY_MAX_M and w.shape[0] % 16 == 0
+    lim = WIDE_MAX_M if (preshuffled and not fp8 and WIDE_MAX_M > SKINNY_MAX_M) else SKINNY_MAX_M
+    return (x.is_cuda and 1 <= m <= lim and w.shape[0] % 16 == 0
             and k % 128 == 0 and x.stride(1) == 1 and w.is_contiguous())
+
+
+def set_wide_plan(waves: int = 0, ksplit: int = 0) -> None:
+    """Override the (waves = 16-column tiles per workgroup, K split) plan of the NEXT wide
+    small-M launch (tuning sweeps); 0 = the kernel library's own plan."""
+    _native().set_wide_plan(int(waves), int(ksplit))
 
 
 def preshuffle(w: torch.Tensor, rowmap: str = "plain") -> torch.Tensor:
@@ -640,11 +656,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = Non
     ``preshuffled``: ``w`` comes from ``preshuffle`` (skinny path only).
     ``w_scale``: ``w`` is fp8 (uint8, ``preshuffle_fp8`` layout) with this per-row scale."""
     _need_cuda(x, preshuffled or w_scale is not None)
-    if w_scale is not None:
+    fp8 = w_scale is not None
+    if fp8:
         preshuffled = True
-    if preshuffled and not skinny_ok(x, w):
+    if preshuffled and not skinny_ok(x, w, preshuffled, fp8):
         raise ValueError("pre-shuffled weights need the skinny (decode) path")
-    if skinny_ok(x, w):
+    if skinny_ok(x, w, preshuffled, fp8):
         ksplit = _ksplit(proj, x, ksplit, w.shape[0] // 16)
         if residual is not None:
             _native().skinny_gemm(residual, x, w, residual, waves or SKINNY_WAVES, preshuffled,

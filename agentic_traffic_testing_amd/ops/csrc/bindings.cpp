@@ -360,6 +360,9 @@ void prefill_gemm_error_to(at::Tensor host, bool clear) {
   check_rc(atta_prefill_gemm_error_async(host.data_ptr(), cur_stream(), clear ? 1 : 0),
            "prefill_gemm_error_to");
 }
+void set_wide_plan(int64_t waves, int64_t ksplit) {
+  atta_set_wide_plan(static_cast<int>(waves), static_cast<int>(ksplit));
+}
 void prefill_gemm_error_reset() {
   check_rc(atta_prefill_gemm_error_reset(), "prefill_gemm_error_reset");
 }
@@ -815,6 +818,7 @@ TORCH_LIBRARY(atta, m) {
   m.def("prefill_gemm_error() -> int", &prefill_gemm_error);
   m.def("prefill_gemm_error_to(Tensor(a!) host, bool clear) -> ()", &prefill_gemm_error_to);
   m.def("prefill_gemm_error_reset() -> ()", &prefill_gemm_error_reset);
+  m.def("set_wide_plan(int waves, int ksplit) -> ()", &set_wide_plan);
   m.def("prefill_gemm_config(int schedule, int group_m, int ablate=0) -> ()", &prefill_gemm_config);
   m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rms_norm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");

@@ -189,6 +189,20 @@ static unsigned long long* take_trace() {
   return t;
 }
 
+// Rows past the 16-row-tile GEMV (33-128, pre-shuffled 16-bit weights) go to the wide
+// small-M kernel (wide.hip); its (waves, split) plan is automatic unless overridden for the
+// NEXT such launch by atta_set_wide_plan (tuning sweeps).
+int atta_wide_launch(SkinnyParams& p, int epi, int ntiles, int waves, int ksplit, int dtype,
+                     const float* sk_ws, int* sk_counters, int64_t ws_floats, int n_counters,
+                     hipStream_t stream);
+static int g_wide_waves = 0, g_wide_ksplit = 0;
+void atta_set_wide_plan(int waves, int ksplit) {
+  g_wide_waves = waves;
+  g_wide_ksplit = ksplit;
+}
+static int wide(SkinnyParams& p, int epi, int ntiles, int dtype, hipStream_t stream);
+static bool use_wide(int M) { return M > 32; }
+
 static int skinny_checks(int M, int K, int waves) {
   if (M < 1 || M > 32) return -1;
   if (K % (32 * waves) != 0) return -1;
@@ -209,6 +223,17 @@ int atta_set_splitk_ws(int device, float* ws, int* counters, int64_t ws_floats, 
   if (device < 0 || device >= 64) return -1;
   g_splitk[device] = SplitKWs{ws, counters, ws_floats, n_counters};
   return 0;
+}
+
+static int wide(SkinnyParams& p, int epi, int ntiles, int dtype, hipStream_t stream) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -2;
+  const SplitKWs& w = g_splitk[dev];
+  const int waves = g_wide_waves, ksplit = g_wide_ksplit;
+  g_wide_waves = g_wide_ksplit = 0;
+  p.wg_trace = take_trace();  // 4 stamps per workgroup here (wide.hip)
+  return atta_wide_launch(p, epi, ntiles, waves, ksplit, dtype, w.ws, w.counters, w.ws_floats,
+                          w.n_counters, stream);
 }
 
 // Resolve the split for one launch: waves fitted to the K slice (fp8: 64-wide granule), the
@@ -239,7 +264,7 @@ int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual
                      int ksplit, const float* wscale, int dtype, hipStream_t stream) {
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
-  if (M < 1 || M > 32 || N % 16 != 0) return -1;
+  if (M < 1 || M > (ps && wscale == nullptr ? 128 : 32) || N % 16 != 0) return -1;
   SkinnyParams p{};
   p.ps = ps;
   p.wscale = wscale;
@@ -250,6 +275,12 @@ int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual
   p.K = K;
   p.x_stride = x_stride;
   p.eps = 0.f;
+  if (use_wide(M)) {
+    if (residual != nullptr && residual != y) return -1;
+    p.y = static_cast<uint16_t*>(y);
+    p.y_stride = residual != nullptr ? res_stride : y_stride;
+    return wide(p, residual != nullptr ? EPI_RESADD : EPI_PLAIN, N / 16, dtype, stream);
+  }
   if (const int rc = setup_split(p, waves, ksplit, N / 16, wscale != nullptr)) return rc;
   const int mt = M <= 16 ? 1 : 2;
   dim3 grid(N / 16, p.ksplit);
@@ -311,7 +342,7 @@ int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x
                         int dtype, hipStream_t stream) {
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
-  if (M < 1 || M > 32) return -1;
+  if (M < 1 || M > (ps && wscale == nullptr ? 128 : 32)) return -1;
   int shift = 0;
   while ((1 << shift) < block_size) ++shift;
   if ((1 << shift) != block_size) return -1;
@@ -335,6 +366,7 @@ int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x
   p.n_q_heads = n_q_heads;
   p.n_kv_heads = n_kv_heads;
   p.bs_shift = shift;
+  if (use_wide(M)) return wide(p, EPI_QKVROPE, p.N / 16, dtype, stream);
   if (const int rc = setup_split(p, waves, ksplit, p.N / 16, wscale != nullptr)) return rc;
   dim3 grid(p.N / 16, p.ksplit);
   p.wg_trace = take_trace();
@@ -347,7 +379,7 @@ int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int 
                             int ksplit, const float* wscale, int dtype, hipStream_t stream) {
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
-  if (M < 1 || M > 32 || inter % 8 != 0) return -1;
+  if (M < 1 || M > (ps && wscale == nullptr ? 128 : 32) || inter % 8 != 0) return -1;
   SkinnyParams p{};
   p.ps = ps;
   p.wscale = wscale;
@@ -361,6 +393,7 @@ int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int 
   p.N = 2 * inter;
   p.inter = inter;
   p.eps = eps;
+  if (use_wide(M)) return wide(p, EPI_SILU, inter / 8, dtype, stream);
   if (const int rc = setup_split(p, waves, ksplit, inter / 8, wscale != nullptr)) return rc;
   dim3 grid(inter / 8, p.ksplit);
   p.wg_trace = take_trace();
@@ -376,7 +409,8 @@ int atta_fused_lm_head_sample(int64_t* tokens, unsigned long long* keys, const v
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
   waves = fit_waves(waves, K, wscale != nullptr);
-  if (skinny_checks(M, K, waves) || N % 16 != 0) return -1;
+  const bool wd = use_wide(M) && ps && wscale == nullptr && M <= 128;
+  if ((!wd && skinny_checks(M, K, waves)) || N % 16 != 0) return -1;
   SkinnyParams p{};
   p.ps = ps;
   p.wscale = wscale;
@@ -395,9 +429,13 @@ int atta_fused_lm_head_sample(int64_t* tokens, unsigned long long* keys, const v
   p.temperature = temperature;
   p.seeds = seeds;
   p.steps = steps;
-  dim3 grid(N / 16);
-  p.wg_trace = take_trace();
-  launch_epi<EPI_SAMPLE>(dtype, M <= 16 ? 1 : 2, waves, grid, stream, p);
+  if (wd) {
+    if (const int rc = wide(p, EPI_SAMPLE, N / 16, dtype, stream)) return rc;
+  } else {
+    dim3 grid(N / 16);
+    p.wg_trace = take_trace();
+    launch_epi<EPI_SAMPLE>(dtype, M <= 16 ? 1 : 2, waves, grid, stream, p);
+  }
   if (finalize == 1)
     sample_finalize_kernel<false><<<M, kFinThreads, 0, stream>>>(tokens, keys, N / 16);
   else if (finalize == 2)

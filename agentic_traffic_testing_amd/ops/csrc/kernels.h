@@ -149,4 +149,5 @@ int atta_prefill_gemm_auto_bm(int M);
 int atta_prefill_gemm_error();
 int atta_prefill_gemm_error_async(void* host, hipStream_t stream, int clear);
 int atta_prefill_gemm_error_reset();
+void atta_set_wide_plan(int waves, int ksplit);
 int atta_prefill_gemm_config(int schedule, int group_m, int ablate);

@@ -127,6 +127,99 @@ __device__ __forceinline__ int tile_row(int tile, int c, const SkinnyParams& p) 
   }
 }
 
+// Epilogue of one 16-column output tile from its fp32 accumulator tile red[row][col] (rows
+// < p.M are valid; inv_rms[row] = the fused RMSNorm scale when norm), run by `nthr` threads
+// (tid = 0..nthr-1): the whole workgroup of the skinny GEMV, or one wave of the wide small-M
+// GEMM (wide.hip).  Rows past p.M are skipped, so MTMAX only bounds the loops.
+template <typename T, int EPI, int MTMAX = 8>
+__device__ __forceinline__ void tile_epilogue(const SkinnyParams& p, const int tile,
+                                              const float (*red)[17], const float* inv_rms,
+                                              const bool norm, const int tid, const int nthr) {
+  if constexpr (EPI == EPI_PLAIN || EPI == EPI_RESADD) {
+    for (int e = tid; e < 16 * 16 * MTMAX; e += nthr) {
+      const int m = e >> 4, n = e & 15;
+      if (m >= p.M) continue;
+      float v = red[m][n];
+      if (norm) v *= inv_rms[m];
+      uint16_t* dst = p.y + static_cast<int64_t>(m) * p.y_stride + tile * 16 + n;
+      if constexpr (EPI == EPI_RESADD) v = to_f32<T>(from_f32<T>(v)) + to_f32<T>(*dst);
+      *dst = from_f32<T>(v);
+    }
+  } else if constexpr (EPI == EPI_SILU) {
+    for (int e = tid; e < 16 * 8 * MTMAX; e += nthr) {
+      const int m = e >> 3, j = e & 7;
+      if (m >= p.M) continue;
+      const float sc = norm ? inv_rms[m] : 1.f;
+      const float g = to_f32<T>(from_f32<T>(red[m][j] * sc));
+      const float u = to_f32<T>(from_f32<T>(red[m][j + 8] * sc));
+      const float si = to_f32<T>(from_f32<T>(g / (1.f + __expf(-g))));
+      p.y[static_cast<int64_t>(m) * p.y_stride + tile * 8 + j] = from_f32<T>(si * u);
+    }
+  } else if constexpr (EPI == EPI_QKVROPE) {
+    const int head = tile >> 3, jb = (tile & 7) * 8;
+    const int nq = p.n_q_heads, nkv = p.n_kv_heads;
+    const int BS = 1 << p.bs_shift;
+    for (int e = tid; e < 16 * 8 * MTMAX; e += nthr) {
+      const int m = e >> 3, c = e & 7;
+      if (m >= p.M) continue;
+      const float sc = norm ? inv_rms[m] : 1.f;
+      // GEMM output rounded to T first (matches the unfused F.linear -> rope path)
+      const float x1 = to_f32<T>(from_f32<T>(red[m][c] * sc));
+      const float x2 = to_f32<T>(from_f32<T>(red[m][c + 8] * sc));
+      const int d = jb + c;  // < 64
+      const int slot = p.slots[m];
+      if (head < nq + nkv) {
+        const float* cs = p.cos_sin + static_cast<int64_t>(p.positions[m]) * 128;
+        const float co = cs[d], si = cs[64 + d];
+        const uint16_t o1 = from_f32<T>(x1 * co - x2 * si);
+        const uint16_t o2 = from_f32<T>(x2 * co + x1 * si);
+        if (head < nq) {
+          uint16_t* q = p.y + static_cast<int64_t>(m) * p.y_stride + head * 128;
+          q[d] = o1;
+          q[d + 64] = o2;
+        } else if (slot >= 0) {
+          const int hk = head - nq;
+          uint16_t* kc = p.k_cache + ((static_cast<int64_t>(slot >> p.bs_shift) * nkv + hk) * BS +
+                                      (slot & (BS - 1))) * 128;
+          kc[d] = o1;
+          kc[d + 64] = o2;
+        }
+      } else if (slot >= 0) {
+        const int hk = head - nq - nkv;
+        uint16_t* vc = p.v_cache + (static_cast<int64_t>(slot >> p.bs_shift) * nkv + hk) * 128 * BS +
+                       (slot & (BS - 1));
+        vc[static_cast<int64_t>(d) * BS] = from_f32<T>(x1);
+        vc[static_cast<int64_t>(d + 64) * BS] = from_f32<T>(x2);
+      }
+    }
+  } else if constexpr (EPI == EPI_SAMPLE) {
+    // one row per thread group of 16 columns: thread e handles (m, n) and reduces over n
+    for (int e = tid; e < 16 * 16 * MTMAX; e += nthr) {
+      const int m = e >> 4, n = e & 15;
+      unsigned long long key = 0ull;
+      if (m < p.M) {
+        const float sc = norm ? inv_rms[m] : 1.f;
+        float v = to_f32<T>(from_f32<T>(red[m][n] * sc));  // bf16 logits, as F.linear
+        const float t = p.temperature[m];
+        const int idx = p.vocab_offset + tile * 16 + n;  // global id: TP == TP1 noise
+        if (t > 1e-5f)
+          v = v / t + gumbel_noise(static_cast<uint64_t>(p.seeds[m]),
+                                   static_cast<uint64_t>(p.steps[m]), static_cast<uint32_t>(idx));
+        key = (static_cast<unsigned long long>(ordered_bits(v)) << 32) |
+              static_cast<unsigned long long>(0xFFFFFFFFu - static_cast<unsigned>(idx));
+      }
+      // max over the 16 columns of this row: lanes e..e+15 are contiguous in a wave
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const unsigned long long other = __shfl_xor(key, o, kWave);
+        key = other > key ? other : key;
+      }
+      // one plain store per (row, tile): no same-address atomics across the ~8k tiles
+      if (n == 0 && m < p.M) p.keys[static_cast<int64_t>(m) * p.key_stride + tile] = key;
+    }
+  }
+}
+
 // Weight layouts.  Row-major [N][K]: a wave's 16-byte-per-lane load touches 16 rows x 64 B
 // (16 DRAM pages per instruction).  Pre-shuffled (PS): for every 16-row tile (rows already
 // permuted by tile_row<EPI>) and every 32-wide K step, the 16 x 32 block is stored as the
@@ -359,89 +452,7 @@ __device__ __forceinline__ void skinny_body(const SkinnyParams& p, const int til
       return;
     }
   }
-  if constexpr (EPI == EPI_PLAIN || EPI == EPI_RESADD) {
-    for (int e = threadIdx.x; e < R * 16; e += WAVES * 64) {
-      const int m = e >> 4, n = e & 15;
-      if (m >= p.M) continue;
-      float v = red[0][m][n];
-      if (norm) v *= inv_rms[m];
-      uint16_t* dst = p.y + static_cast<int64_t>(m) * p.y_stride + tile * 16 + n;
-      if constexpr (EPI == EPI_RESADD) v = to_f32<T>(from_f32<T>(v)) + to_f32<T>(*dst);
-      *dst = from_f32<T>(v);
-    }
-  } else if constexpr (EPI == EPI_SILU) {
-    for (int e = threadIdx.x; e < R * 8; e += WAVES * 64) {
-      const int m = e >> 3, j = e & 7;
-      if (m >= p.M) continue;
-      const float sc = norm ? inv_rms[m] : 1.f;
-      const float g = to_f32<T>(from_f32<T>(red[0][m][j] * sc));
-      const float u = to_f32<T>(from_f32<T>(red[0][m][j + 8] * sc));
-      const float si = to_f32<T>(from_f32<T>(g / (1.f + __expf(-g))));
-      p.y[static_cast<int64_t>(m) * p.y_stride + tile * 8 + j] = from_f32<T>(si * u);
-    }
-  } else if constexpr (EPI == EPI_QKVROPE) {
-    const int head = tile >> 3, jb = (tile & 7) * 8;
-    const int nq = p.n_q_heads, nkv = p.n_kv_heads;
-    const int BS = 1 << p.bs_shift;
-    for (int e = threadIdx.x; e < R * 8; e += WAVES * 64) {
-      const int m = e >> 3, c = e & 7;
-      if (m >= p.M) continue;
-      const float sc = norm ? inv_rms[m] : 1.f;
-      // GEMM output rounded to T first (matches the unfused F.linear -> rope path)
-      const float x1 = to_f32<T>(from_f32<T>(red[0][m][c] * sc));
-      const float x2 = to_f32<T>(from_f32<T>(red[0][m][c + 8] * sc));
-      const int d = jb + c;  // < 64
-      const int slot = p.slots[m];
-      if (head < nq + nkv) {
-        const float* cs = p.cos_sin + static_cast<int64_t>(p.positions[m]) * 128;
-        const float co = cs[d], si = cs[64 + d];
-        const uint16_t o1 = from_f32<T>(x1 * co - x2 * si);
-        const uint16_t o2 = from_f32<T>(x2 * co + x1 * si);
-        if (head < nq) {
-          uint16_t* q = p.y + static_cast<int64_t>(m) * p.y_stride + head * 128;
-          q[d] = o1;
-          q[d + 64] = o2;
-        } else if (slot >= 0) {
-          const int hk = head - nq;
-          uint16_t* kc = p.k_cache + ((static_cast<int64_t>(slot >> p.bs_shift) * nkv + hk) * BS +
-                                      (slot & (BS - 1))) * 128;
-          kc[d] = o1;
-          kc[d + 64] = o2;
-        }
-      } else if (slot >= 0) {
-        const int hk = head - nq - nkv;
-        uint16_t* vc = p.v_cache + (static_cast<int64_t>(slot >> p.bs_shift) * nkv + hk) * 128 * BS +
-                       (slot & (BS - 1));
-        vc[static_cast<int64_t>(d) * BS] = from_f32<T>(x1);
-        vc[static_cast<int64_t>(d + 64) * BS] = from_f32<T>(x2);
-      }
-    }
-  } else if constexpr (EPI == EPI_SAMPLE) {
-    // one row per thread group of 16 columns: thread e handles (m, n) and reduces over n
-    for (int e = threadIdx.x; e < R * 16; e += WAVES * 64) {
-      const int m = e >> 4, n = e & 15;
-      unsigned long long key = 0ull;
-      if (m < p.M) {
-        const float sc = norm ? inv_rms[m] : 1.f;
-        float v = to_f32<T>(from_f32<T>(red[0][m][n] * sc));  // bf16 logits, as F.linear
-        const float t = p.temperature[m];
-        const int idx = p.vocab_offset + tile * 16 + n;  // global id: TP == TP1 noise
-        if (t > 1e-5f)
-          v = v / t + gumbel_noise(static_cast<uint64_t>(p.seeds[m]),
-                                   static_cast<uint64_t>(p.steps[m]), static_cast<uint32_t>(idx));
-        key = (static_cast<unsigned long long>(ordered_bits(v)) << 32) |
-              static_cast<unsigned long long>(0xFFFFFFFFu - static_cast<unsigned>(idx));
-      }
-      // max over the 16 columns of this row: lanes e..e+15 are contiguous in a wave
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        const unsigned long long other = __shfl_xor(key, o, kWave);
-        key = other > key ? other : key;
-      }
-      // one plain store per (row, tile): no same-address atomics across the ~8k tiles
-      if (n == 0 && m < p.M) p.keys[static_cast<int64_t>(m) * p.key_stride + tile] = key;
-    }
-  }
+  tile_epilogue<T, EPI, MT>(p, tile, red[0], inv_rms, norm, threadIdx.x, WAVES * 64);
 }
 
 }  // namespace atta

@@ -1,0 +1,113 @@
+"""Wide small-M GEMM (ops/csrc/wide.hip) vs the library at the Llama-3.1-8B projection shapes:
+us per call and weight-stream TB/s, cold weights (rotating copies past the 256 MB Infinity
+Cache), with the fused epilogues the engine uses (qkv: norm + RoPE + K/V write, o / down:
+residual add, gate_up: norm + SiLU-mul).  Library column = F.linear (hipBLASLt) on row-major
+weights plus the separate norm / RoPE / SiLU kernels it needs.
+
+    python scripts/gpu/bench_wide.py [--m 33 85 128] [--plans]
+"""
+import argparse
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+from agentic_traffic_testing_amd import ops  # noqa: E402
+from agentic_traffic_testing_amd.ops import reference as ref  # noqa: E402
+
+SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+PLANS = {"qkv": [(6, 4), (8, 4), (6, 2), (4, 4), (8, 6)],
+         "o": [(8, 8), (4, 4), (8, 4), (4, 8), (6, 6)],
+         "gate_up": [(7, 1), (8, 1), (4, 1), (4, 2), (8, 2)],
+         "down": [(8, 8), (4, 4), (8, 4), (4, 8), (8, 16)]}
+
+
+def timeit(fn, n=30, reps=3):
+    for i in range(3):
+        fn(i)
+    torch.cuda.synchronize()
+    out = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(n):
+            fn(i)
+        e1.record()
+        torch.cuda.synchronize()
+        out.append(e0.elapsed_time(e1) * 1e3 / n)
+    return statistics.median(out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", type=int, nargs="+", default=[33, 48, 64, 85, 96, 128])
+    ap.add_argument("--plans", action="store_true", help="also sweep (waves, split) plans")
+    ap.add_argument("--proj", nargs="+", default=list(SHAPES))
+    a = ap.parse_args()
+    assert ops.native_available(), ops._load_error
+    ops.ensure_splitk_workspace("cuda")
+    dt = torch.bfloat16
+    hq, hkv, bs, nb = 32, 8, 16, 512
+    kc = torch.zeros(nb, hkv, bs, 128, dtype=dt, device="cuda")
+    vc = torch.zeros(nb, hkv, 128, bs, dtype=dt, device="cuda")
+    cs = ref.rope_cos_sin(128, 8192, 500000.0, None, device="cuda")
+    ones = torch.ones(4096, dtype=dt, device="cuda")
+    tot = {}
+    for proj in a.proj:
+        n, k = SHAPES[proj]
+        mb = n * k * 2 / 1e6
+        ncopy = max(2, int(600 // mb) + 1)
+        rowmap = {"qkv": "qkv", "gate_up": "silu"}.get(proj, "plain")
+        raw = [(torch.randn(n, k, device="cuda") * 0.02).to(dt) for _ in range(ncopy)]
+        wps = [ops.preshuffle(w, rowmap) for w in raw]
+        for m in a.m:
+            x = torch.randn(m, k, device="cuda").to(dt)
+            res = torch.zeros(m, n, dtype=dt, device="cuda")
+            pos = torch.arange(m, dtype=torch.int32, device="cuda")
+            slots = torch.arange(m, dtype=torch.int32, device="cuda")
+            q = torch.empty(m, hq, 128, dtype=dt, device="cuda")
+            act = torch.empty(m, n // 2, dtype=dt, device="cuda")
+
+            def wide(i, plan=(0, 0)):
+                ops.set_wide_plan(*plan)
+                w = wps[i % ncopy]
+                if proj == "qkv":
+                    ops.decode_qkv_rope(x, w, 1e-5, pos, slots, cs, kc, vc, hq, hkv, q_out=q,
+                                        preshuffled=True)
+                elif proj == "gate_up":
+                    ops.decode_gate_up_silu(x, w, 1e-5, out=act, preshuffled=True)
+                else:
+                    ops.linear(x, w, residual=res, preshuffled=True)
+
+            def lib(i):
+                w = raw[i % ncopy]
+                if proj == "qkv":
+                    y = torch.nn.functional.linear(ops.rms_norm(x, ones, 1e-5), w)
+                    ops.rope_cache(y, pos, slots, cs, kc, vc, hq, hkv, 128)
+                elif proj == "gate_up":
+                    ops.silu_and_mul(torch.nn.functional.linear(ops.rms_norm(x, ones, 1e-5), w))
+                else:
+                    res.addmm_(x, w.t())
+
+            tw = timeit(wide)
+            tl = timeit(lib)
+            tot.setdefault(m, [0.0, 0.0])
+            tot[m][0] += tw
+            tot[m][1] += tl
+            line = (f"{proj:8s} M={m:4d} | wide {tw:7.1f} us ({mb / tw:5.2f} TB/s) | "
+                    f"library {tl:7.1f} us | {tl / tw:5.2f}x")
+            if a.plans:
+                line += " | plans " + " ".join(
+                    f"{w_}x{s_}={timeit(lambda i, p=(w_, s_): wide(i, p)):.1f}"
+                    for w_, s_ in PLANS[proj])
+            print(line, flush=True)
+        del raw, wps
+        torch.cuda.empty_cache()
+    for m, (tw, tl) in tot.items():
+        print(f"per layer M={m}: wide {tw:7.1f} us, library {tl:7.1f} us ({tl / tw:.2f}x)")
+
+
+if __name__ == "__main__":
+    main()

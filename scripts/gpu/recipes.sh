@@ -12,6 +12,7 @@
 #   refresh      HTTP fan-out, 8B fp8, 70B fp8 TP=1 benches (r4_final_secondary.log)
 #   tp8          TP=8 rehearsal (8 ranks on one GPU) with graph node dumps, push on / off, and the
 #                AgentVerse HTTP runs on 8B and 70B fp8 (r4_tp8_*, r4_http_agentverse_*)
+#   tp8fp8       TP=8 x fp8 rehearsal (8 ranks on one GPU, fused push, graph steps in the JSON line)
 #   largem       large-M GEMM routing A/B vs the tuned library table (r4_prefill_gemm_largem_ab.txt)
 #   flash        flash-prefill tests, microbench, elementwise probe, PMC passes (r4_flash_prefill_rework.txt)
 #   burst        windowed profile of the 380-row burst prefill (r4_prof_burst380_summary.txt)
@@ -42,6 +43,10 @@ recipe() {
       rm -rf gpurun_out/graphs_push gpurun_out/graphs_nopush &&
       TAG=r4av8b STAGES=http STEPS=1 BENCH_ARGS="--workload agentverse" bash $S &&
       TAG=r4av70b STAGES=http STEPS=1 BENCH_ARGS="--workload agentverse --model llama-3-70b --quantization fp8" bash $S ;;
+    tp8fp8)
+      # BASELINE config 5 rehearsal: 8 TP ranks on one GPU, fp8 weights, fused push, graphs
+      TAG=r5tp8fp8 STAGES=bench STEPS=1 BENCH_ARGS="--gpus 8 --parallel tp --tp-same-device \
+        --model llama-70b-tp-slice-fp8 --quantization fp8 --max-tokens 64" bash $S ;;
     largem)
       TAG=r4lm_bf16 STAGES=gemm GEMM_ARGS="--m 2048 2560 3200 4096 --tuned auto --rounds 3" bash $S &&
       TAG=r4lm_fp8 STAGES=gemm GEMM_ARGS="--m 512 1024 2048 3200 --fp8 --rounds 3" bash $S ;;

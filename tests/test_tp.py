@@ -350,7 +350,7 @@ def test_tp_same_gpu_graph_captured_decode(tp, model, push):
 @pytest.mark.parametrize("tp", [4, 8])
 def test_tp_fp8_same_gpu_graph_captured_decode(tp):
     """BASELINE config 5 (TP x fp8) as a same-GPU rehearsal on the 70B TP=8
-    per-rank geometry slice: fp8 weight-only GEMVs on every rank, the all-reduce push fused
+    per-rank geometry slice (FFN shard a multiple of the fp8 GEMV's 256-wide K step): fp8 weight-only GEMVs on every rank, the all-reduce push fused
     into the o / down fp8 GEMV epilogues, graph-captured decode.  Greedy tokens match TP=1 fp8
     (same fp8 weights bit for bit: row-parallel shards quantise with the full-row scale) up
     to near ties, >= 95 % of decode steps replay from graphs, IPC word stays 0.
@@ -362,7 +362,7 @@ def test_tp_fp8_same_gpu_graph_captured_decode(tp):
     most one divergent position in five), not token-for-token against TP=1."""
     from helpers import dense_logits_fp8
 
-    base = dict(model="llama-70b-tp-slice", device="cuda:0", max_model_len=512,
+    base = dict(model="llama-70b-tp-slice-fp8", device="cuda:0", max_model_len=512,
                 num_kv_blocks=128, max_num_batched_tokens=256, max_num_seqs=4,
                 use_graphs=True, quantization="fp8")
     greedy = SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True)
