@@ -187,9 +187,14 @@ def run_e2e(engine, steps: int, warmup: int, fanout: int = 5, max_tokens: int = 
         "p50_ttft_burst_s": med(r["queue_wait_s"] for r in recs if r.get("burst")),
         "p50_ttft_solo_s": med(r["queue_wait_s"] for r in recs if not r.get("burst")),
         "p50_hold_burst_s": med(r.get("hold_s", 0.0) for r in recs if r.get("burst")),
-        # engine clock: arrival -> scheduled, scheduled -> first token; the rest of the HTTP
-        # TTFT is the engine-thread -> event-loop hand-off
+        # engine clock: arrival -> scheduled (INCLUDES the hold), scheduled -> first token;
+        # the rest of the HTTP TTFT is the engine-thread -> event-loop hand-off.  The parts
+        # add up as ttft = sched_wait + prefill + handoff, with sched_wait = hold + the wait
+        # between the burst's release and its first engine step (p50_admit_wait_burst_s)
         "p50_sched_wait_burst_s": med(r["sched_wait_s"] for r in recs
+                                      if r.get("burst") and r.get("sched_wait_s") is not None),
+        "p50_admit_wait_burst_s": med(max(0.0, r["sched_wait_s"] - r.get("hold_s", 0.0))
+                                      for r in recs
                                       if r.get("burst") and r.get("sched_wait_s") is not None),
         "p50_prefill_burst_s": med(r["engine_ttft_s"] - r["sched_wait_s"] for r in recs
                                    if r.get("burst") and r.get("engine_ttft_s") is not None

@@ -91,6 +91,11 @@ struct SkinnyParams {
   int ksplit;
   float* sk_ws;
   int* sk_counters;
+  // tail split (gridDim.y == 1): tiles below split_from run unsplit, the remaining tiles
+  // ksplit ways - a grid of tiles that is not a multiple of the CU count (qkv: 384 tiles on
+  // 256 CUs) gets its last partial round spread over every CU instead of doubling half of
+  // them.  0 = off (every tile split ksplit ways along gridDim.y)
+  int split_from;
   // optional per-workgroup timeline (ops.set_gemv_trace): [start, end] on the 100 MHz wall
   // clock per workgroup of the grid (gridDim.y == 1 launches only)
   unsigned long long* wg_trace;
@@ -233,7 +238,8 @@ __device__ __forceinline__ void tile_epilogue(const SkinnyParams& p, const int t
 // per-row scale multiplies the reduced accumulator.  Halves the weight stream.
 template <typename T, int WAVES, int UNROLL, int MT, int EPI, bool NTL = false, bool PS = false,
           bool W8 = false>
-__device__ __forceinline__ void skinny_body(const SkinnyParams& p, const int tile, const int ks) {
+__device__ __forceinline__ void skinny_body(const SkinnyParams& p, const int tile, const int ks,
+                                            const int ksplit) {
   static_assert(!W8 || (UNROLL % 2 == 0), "fp8 weights load K-step pairs");
   using MF = MfmaK32<T>;
   using frag8 = typename MF::frag8;
@@ -247,7 +253,7 @@ __device__ __forceinline__ void skinny_body(const SkinnyParams& p, const int til
   const int wid = threadIdx.x >> 6;
   const int col = lane & 15;
   const int grp = lane >> 4;
-  const int kslice = p.K / p.ksplit;
+  const int kslice = p.K / ksplit;
   const int kw = kslice / WAVES;
   const int kbeg = ks * kslice + wid * kw;
   const int wrow = tile_row<EPI>(tile, col, p);
@@ -383,12 +389,12 @@ __device__ __forceinline__ void skinny_body(const SkinnyParams& p, const int til
     red[0][m][n] = s;
   }
   __syncthreads();
-  if (p.ksplit > 1) {
+  if (ksplit > 1) {
     // ---- split-K hand-over (device-scope sc1 stores/loads + arrival counter, no fences:
     // common.h "device-coherent hand-over"); slot = R*16 partial sums + R row sums of squares
     constexpr int kSlot = R * 16 + R;
     const auto rws = dev_rsrc(p.sk_ws);
-    const uint32_t mine = static_cast<uint32_t>((tile * p.ksplit + ks) * kSlot) * 4u;
+    const uint32_t mine = static_cast<uint32_t>((tile * ksplit + ks) * kSlot) * 4u;
     for (int e = threadIdx.x; e < R * 16; e += WAVES * 64)
       if ((e >> 4) < p.M) dev_store4(rws, mine + e * 4, red[0][e >> 4][e & 15]);
     if (norm && threadIdx.x < R && threadIdx.x < p.M)
@@ -398,20 +404,20 @@ __device__ __forceinline__ void skinny_body(const SkinnyParams& p, const int til
     if (threadIdx.x == 0) {
       const int old = __hip_atomic_fetch_add(p.sk_counters + tile, 1, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
-      sk_last = (old == p.ksplit - 1);
+      sk_last = (old == ksplit - 1);
     }
     __syncthreads();
     if (!sk_last) return;  // block-uniform
-    const uint32_t first = static_cast<uint32_t>(tile * p.ksplit * kSlot) * 4u;
+    const uint32_t first = static_cast<uint32_t>(tile * ksplit * kSlot) * 4u;
     for (int e = threadIdx.x; e < R * 16; e += WAVES * 64) {
       if ((e >> 4) >= p.M) continue;
       float s = 0.f;
-      for (int q = 0; q < p.ksplit; ++q) s += dev_load4(rws, first + (q * kSlot + e) * 4);
+      for (int q = 0; q < ksplit; ++q) s += dev_load4(rws, first + (q * kSlot + e) * 4);
       red[0][e >> 4][e & 15] = s;
     }
     if (norm && threadIdx.x < R && threadIdx.x < p.M) {
       float s = 0.f;
-      for (int q = 0; q < p.ksplit; ++q)
+      for (int q = 0; q < ksplit; ++q)
         s += dev_load4(rws, first + (q * kSlot + R * 16 + threadIdx.x) * 4);
       inv_rms[threadIdx.x] = s;
     }

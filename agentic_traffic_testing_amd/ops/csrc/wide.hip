@@ -39,7 +39,174 @@ constexpr int kKC = 128;             // K columns per staged chunk (4 MFMA K ste
 constexpr int kRowB = kKC * 2;       // bytes of one staged x row
 constexpr int kSlots = kRowB / 16;   // 16-B slots per staged row
 
-template <typename T, int WAVES, int MT, int EPI>
+// Epilogue of one wave's 16-column tile, one accumulator ROW per lane (rows lane and lane + 64):
+// every global load of a row (residual segment, position / slot / cos-sin, sampler params) is
+// issued before any of its uses and rows move as 16-B vectors.  (The element-per-thread
+// tile_epilogue of the GEMV, run by one wave over up to 128 rows, paid one dependent load
+// round trip per element: 24 serialized residual loads per wave at 96 rows.)
+template <typename T, int EPI, int MT>
+__device__ __forceinline__ void row_epilogue(const SkinnyParams& p, const int tile,
+                                             const float (*red)[17], const float* inv_rms,
+                                             const bool norm, const int lane) {
+  constexpr int RPL = MT * 16 > 64 ? 2 : 1;  // rows per lane
+  int rows[RPL];
+  bool ok[RPL];
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    rows[j] = lane + 64 * j;
+    ok[j] = rows[j] < MT * 16 && rows[j] < p.M;
+  }
+  if constexpr (EPI == EPI_PLAIN || EPI == EPI_RESADD) {
+    u32x4 res[RPL][2];
+    if constexpr (EPI == EPI_RESADD) {
+#pragma unroll
+      for (int j = 0; j < RPL; ++j) {
+        const u32x4* src = reinterpret_cast<const u32x4*>(
+            p.y + static_cast<int64_t>(ok[j] ? rows[j] : 0) * p.y_stride + tile * 16);
+        res[j][0] = src[0];
+        res[j][1] = src[1];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      if (!ok[j]) continue;
+      const int m = rows[j];
+      const float sc = norm ? inv_rms[m] : 1.f;
+      uint16_t o[16];
+#pragma unroll
+      for (int n = 0; n < 16; ++n) {
+        float v = red[m][n] * sc;
+        if constexpr (EPI == EPI_RESADD) {
+          const uint32_t w = res[j][n >> 3][(n >> 1) & 3];
+          v = to_f32<T>(from_f32<T>(v)) + to_f32<T>(static_cast<uint16_t>((n & 1) ? w >> 16 : w));
+        }
+        o[n] = from_f32<T>(v);
+      }
+      u32x4* dst = reinterpret_cast<u32x4*>(p.y + static_cast<int64_t>(m) * p.y_stride + tile * 16);
+      dst[0] = u32x4{o[0] | (uint32_t(o[1]) << 16), o[2] | (uint32_t(o[3]) << 16),
+                     o[4] | (uint32_t(o[5]) << 16), o[6] | (uint32_t(o[7]) << 16)};
+      dst[1] = u32x4{o[8] | (uint32_t(o[9]) << 16), o[10] | (uint32_t(o[11]) << 16),
+                     o[12] | (uint32_t(o[13]) << 16), o[14] | (uint32_t(o[15]) << 16)};
+    }
+  } else if constexpr (EPI == EPI_SILU) {
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      if (!ok[j]) continue;
+      const int m = rows[j];
+      const float sc = norm ? inv_rms[m] : 1.f;
+      uint16_t o[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float g = to_f32<T>(from_f32<T>(red[m][c] * sc));
+        const float u = to_f32<T>(from_f32<T>(red[m][c + 8] * sc));
+        const float si = to_f32<T>(from_f32<T>(g / (1.f + __expf(-g))));
+        o[c] = from_f32<T>(si * u);
+      }
+      *reinterpret_cast<u32x4*>(p.y + static_cast<int64_t>(m) * p.y_stride + tile * 8) =
+          u32x4{o[0] | (uint32_t(o[1]) << 16), o[2] | (uint32_t(o[3]) << 16),
+                o[4] | (uint32_t(o[5]) << 16), o[6] | (uint32_t(o[7]) << 16)};
+    }
+  } else if constexpr (EPI == EPI_QKVROPE) {
+    const int head = tile >> 3, jb = (tile & 7) * 8;
+    const int nq = p.n_q_heads, nkv = p.n_kv_heads;
+    const int BS = 1 << p.bs_shift;
+    int pos[RPL], slot[RPL];
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      const int m = ok[j] ? rows[j] : 0;
+      pos[j] = p.positions[m];
+      slot[j] = p.slots[m];
+    }
+    f32x4 cs[RPL][4];  // cos d..d+7, sin d..d+7
+    if (head < nq + nkv) {
+#pragma unroll
+      for (int j = 0; j < RPL; ++j) {
+        const f32x4* c4 = reinterpret_cast<const f32x4*>(p.cos_sin + static_cast<int64_t>(pos[j]) * 128 + jb);
+        cs[j][0] = c4[0];
+        cs[j][1] = c4[1];
+        cs[j][2] = c4[16];  // + 64 floats
+        cs[j][3] = c4[17];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      if (!ok[j]) continue;
+      const int m = rows[j];
+      const float sc = norm ? inv_rms[m] : 1.f;
+      uint16_t o1[8], o2[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        // GEMM output rounded to T first (matches the unfused F.linear -> rope path)
+        const float x1 = to_f32<T>(from_f32<T>(red[m][c] * sc));
+        const float x2 = to_f32<T>(from_f32<T>(red[m][c + 8] * sc));
+        if (head < nq + nkv) {
+          const float co = cs[j][c >> 2][c & 3], si = cs[j][2 + (c >> 2)][c & 3];
+          o1[c] = from_f32<T>(x1 * co - x2 * si);
+          o2[c] = from_f32<T>(x2 * co + x1 * si);
+        } else {
+          o1[c] = from_f32<T>(x1);
+          o2[c] = from_f32<T>(x2);
+        }
+      }
+      const u32x4 v1 = {o1[0] | (uint32_t(o1[1]) << 16), o1[2] | (uint32_t(o1[3]) << 16),
+                        o1[4] | (uint32_t(o1[5]) << 16), o1[6] | (uint32_t(o1[7]) << 16)};
+      const u32x4 v2 = {o2[0] | (uint32_t(o2[1]) << 16), o2[2] | (uint32_t(o2[3]) << 16),
+                        o2[4] | (uint32_t(o2[5]) << 16), o2[6] | (uint32_t(o2[7]) << 16)};
+      if (head < nq) {
+        uint16_t* q = p.y + static_cast<int64_t>(m) * p.y_stride + head * 128 + jb;
+        *reinterpret_cast<u32x4*>(q) = v1;
+        *reinterpret_cast<u32x4*>(q + 64) = v2;
+      } else if (slot[j] >= 0) {
+        const int sl = slot[j];
+        if (head < nq + nkv) {
+          uint16_t* kc = p.k_cache + ((static_cast<int64_t>(sl >> p.bs_shift) * nkv + (head - nq)) * BS +
+                                      (sl & (BS - 1))) * 128 + jb;
+          *reinterpret_cast<u32x4*>(kc) = v1;
+          *reinterpret_cast<u32x4*>(kc + 64) = v2;
+        } else {
+          uint16_t* vc = p.v_cache + (static_cast<int64_t>(sl >> p.bs_shift) * nkv + (head - nq - nkv)) *
+                                         128 * BS + (sl & (BS - 1));
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            vc[static_cast<int64_t>(jb + c) * BS] = o1[c];
+            vc[static_cast<int64_t>(jb + c + 64) * BS] = o2[c];
+          }
+        }
+      }
+    }
+  } else if constexpr (EPI == EPI_SAMPLE) {
+    float temp[RPL];
+    uint64_t seed[RPL], step[RPL];
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      const int m = ok[j] ? rows[j] : 0;
+      temp[j] = p.temperature[m];
+      seed[j] = static_cast<uint64_t>(p.seeds[m]);
+      step[j] = static_cast<uint64_t>(p.steps[m]);
+    }
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      if (!ok[j]) continue;
+      const int m = rows[j];
+      const float sc = norm ? inv_rms[m] : 1.f;
+      unsigned long long best = 0ull;
+#pragma unroll
+      for (int n = 0; n < 16; ++n) {
+        float v = to_f32<T>(from_f32<T>(red[m][n] * sc));  // bf16 logits, as F.linear
+        const int idx = p.vocab_offset + tile * 16 + n;    // global id: TP == TP1 noise
+        if (temp[j] > 1e-5f)
+          v = v / temp[j] + gumbel_noise(seed[j], step[j], static_cast<uint32_t>(idx));
+        const unsigned long long key =
+            (static_cast<unsigned long long>(ordered_bits(v)) << 32) |
+            static_cast<unsigned long long>(0xFFFFFFFFu - static_cast<unsigned>(idx));
+        best = key > best ? key : best;
+      }
+      p.keys[static_cast<int64_t>(m) * p.key_stride + tile] = best;
+    }
+  }
+}
+
+template <typename T, int WAVES, int MT, int EPI, bool NORM>
 __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int ntiles) {
   using MF = MfmaK32<T>;
   using frag8 = typename MF::frag8;
@@ -70,13 +237,13 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
   const bool tvalid = tile < ntiles;
   const int nch = p.K / kKC;
   const int c0 = ks * nch / S, c1 = (ks + 1) * nch / S;
-  const bool norm = p.eps > 0.f;
+  constexpr bool norm = NORM;  // p.eps > 0: fused RMSNorm (compile-time: no branches in the loop)
 
   // this wave's weight tile (idle waves of the last column block stream tile 0 and store
   // nothing: every wave takes part in the barriers)
   const uint16_t* wp = p.w + static_cast<int64_t>(tvalid ? tile : 0) * (p.K / 32) * 512 + lane * 8;
   // x pieces of this thread: piece q = tid + i * NTHR -> staged row q / 16, slot q % 16
-  const uint16_t* xsrc[PPT];
+  int xsrc[PPT];  // element offsets from p.x (32-bit: x is < 4 MB here)
   int xdst[PPT];
   bool xst[PPT], xss[PPT];
 #pragma unroll
@@ -84,10 +251,10 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
     const int q = tid + i * NTHR;
     const int row = q < PIECES ? q / kSlots : 0;
     const int slot = q % kSlots;
-    xst[i] = q < PIECES;
+    xst[i] = q < PIECES;  // only the last piece can be out of range (PIECES % NTHR != 0)
     xss[i] = q < PIECES && row < p.M;
     // rows past M stage a copy of row M - 1 (finite; their accumulator rows are discarded)
-    xsrc[i] = p.x + static_cast<int64_t>(min(row, p.M - 1)) * p.x_stride + slot * 8;
+    xsrc[i] = min(row, p.M - 1) * static_cast<int>(p.x_stride) + slot * 8;
     xdst[i] = row * kRowB + ((slot ^ (row & 15)) << 4);
   }
 
@@ -110,17 +277,24 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
   };
   auto load_x = [&](u32x4 (&xr)[PPT], int c) {
 #pragma unroll
-    for (int i = 0; i < PPT; ++i) xr[i] = *reinterpret_cast<const u32x4*>(xsrc[i] + c * kKC);
+    for (int i = 0; i < PPT; ++i) xr[i] = *reinterpret_cast<const u32x4*>(p.x + xsrc[i] + c * kKC);
   };
-  auto store_x = [&](const u32x4 (&xr)[PPT], int buf) {
+  // no data-dependent control flow around the staging: branches between the loads and their
+  // uses made hipcc's waitcnt pass fall back to near-vmcnt(0) waits at every block join
+  auto store_x = [&](const u32x4 (&xr)[PPT], int buf, bool real) {
     unsigned char* b = lds + buf * XBUF;
 #pragma unroll
-    for (int i = 0; i < PPT; ++i)
-      if (xst[i]) *reinterpret_cast<u32x4*>(b + xdst[i]) = xr[i];
-    if (norm) {
+    for (int i = 0; i < PPT; ++i) {
+      if (PIECES % NTHR == 0 || i + 1 < PPT || xst[i])
+        *reinterpret_cast<u32x4*>(b + xdst[i]) = xr[i];
+    }
+    if constexpr (norm) {
 #pragma unroll
-      for (int i = 0; i < PPT; ++i)
-        if (xss[i]) ss[i] = MF::sq8(__builtin_bit_cast(frag8, xr[i]), ss[i]);
+      for (int i = 0; i < PPT; ++i) {
+        // rows past M (and an out-of-range last piece) add 0: the select keeps it branch-free
+        const float v = MF::sq8(__builtin_bit_cast(frag8, xr[i]), 0.f);
+        ss[i] += (xss[i] && real) ? v : 0.f;
+      }
     }
   };
   auto compute = [&](const u32x4 (&f)[4], int buf) {
@@ -136,40 +310,55 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
       }
     }
   };
-  // one chunk: issue chunk c + 2's loads, compute chunk c, stage chunk c + 1's x, barrier
+  // one chunk: issue chunk c + 2's loads, compute chunk c, stage chunk c + 1's x, barrier.
+  // Past the slice end the loads re-read the slice's last chunk and the staging writes the
+  // idle buffer (never computed): unconditional, so the loop body has no branches.
+  const int clast = c1 - 1;
   auto iter = [&](const u32x4 (&wcur)[4], u32x4 (&wnext)[4], const u32x4 (&xstage)[PPT],
                   u32x4 (&xload)[PPT], int c, int buf) {
-    if (c + 2 < c1) {
-      load_x(xload, c + 2);
-      load_w(wnext, c + 2);
-    }
+    load_x(xload, min(c + 2, clast));
+    load_w(wnext, min(c + 2, clast));
     compute(wcur, buf);
-    if (c + 1 < c1) store_x(xstage, buf ^ 1);
-    __syncthreads();
+    store_x(xstage, buf ^ 1, c + 1 < c1);  // past the end: a re-staged chunk, no squares
+    // LDS hand-over only: ds_writes retired, then a bare s_barrier - __syncthreads()' fence
+    // semantics made hipcc drain the weight / x loads in flight (vmcnt(0)) at the period's
+    // loop header
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
   };
 
   if (c0 < c1) {
     load_x(xa, c0);
     load_w(w0, c0);
-    if (c0 + 1 < c1) {
-      load_x(xb, c0 + 1);
-      load_w(w1, c0 + 1);
-    }
-    store_x(xa, 0);
+    load_x(xb, min(c0 + 1, clast));
+    load_w(w1, min(c0 + 1, clast));
+    store_x(xa, 0, true);
   }
   __syncthreads();
-  for (int c = c0; c < c1; c += 6) {
+  // whole 6-chunk periods (3 weight stages x 2 x sets) with no exits inside the loop body, then
+  // the <= 5 remaining chunks
+  int c = c0;
+  for (; c + 6 <= c1; c += 6) {
     iter(w0, w2, xb, xa, c, 0);
-    if (c + 1 >= c1) break;
     iter(w1, w0, xa, xb, c + 1, 1);
-    if (c + 2 >= c1) break;
     iter(w2, w1, xb, xa, c + 2, 0);
-    if (c + 3 >= c1) break;
     iter(w0, w2, xa, xb, c + 3, 1);
-    if (c + 4 >= c1) break;
     iter(w1, w0, xb, xa, c + 4, 0);
-    if (c + 5 >= c1) break;
     iter(w2, w1, xa, xb, c + 5, 1);
+  }
+  if (c < c1) {
+    iter(w0, w2, xb, xa, c, 0);
+    if (c + 1 < c1) {
+      iter(w1, w0, xa, xb, c + 1, 1);
+      if (c + 2 < c1) {
+        iter(w2, w1, xb, xa, c + 2, 0);
+        if (c + 3 < c1) {
+          iter(w0, w2, xa, xb, c + 3, 1);
+          if (c + 4 < c1) iter(w1, w0, xb, xa, c + 4, 0);
+        }
+      }
+    }
   }
 
   if (p.wg_trace != nullptr) tr1 = tr2 = wall_clock64();
@@ -221,20 +410,34 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
     }
     const uint32_t first = static_cast<uint32_t>(cb * S) * per_slice +
                            static_cast<uint32_t>(wid * R * 16 + col * R + 4 * grp);
-    f32x4 part[MT];
+    // QB slices' partials in flight per round trip (<= 16 16-B loads per lane), summed in
+    // slice order: deterministic
+    constexpr int QB = MT <= 2 ? 8 : MT <= 4 ? 4 : 2;
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int q = 0; q < S; ++q) {  // slice order: deterministic sums
+    for (int q0 = 0; q0 < S; q0 += QB) {
+      f32x4 part[QB][MT];
 #pragma unroll
-      for (int t = 0; t < MT; ++t)
-        part[t] = __builtin_bit_cast(f32x4, dev_load16(rws, (first + q * per_slice + 16 * t) * 4u));
+      for (int u = 0; u < QB; ++u) {
+        const int q = min(q0 + u, S - 1);
 #pragma unroll
-      for (int t = 0; t < MT; ++t) acc[t] += part[t];
+        for (int t = 0; t < MT; ++t)
+          part[u][t] = __builtin_bit_cast(
+              f32x4, dev_load16(rws, (first + q * per_slice + 16 * t) * 4u));
+      }
+#pragma unroll
+      for (int u = 0; u < QB; ++u)
+#pragma unroll
+        for (int t = 0; t < MT; ++t) acc[t] += (q0 + u < S) ? part[u][t] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     if (norm && tid < R) {
+      float part[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        part[u] = dev_load4(rws, (ss_base + static_cast<uint32_t>((cb * S + min(u, S - 1)) * R + tid)) * 4u);
       float sum = 0.f;
-      for (int q = 0; q < S; ++q)
-        sum += dev_load4(rws, (ss_base + static_cast<uint32_t>((cb * S + q) * R + tid)) * 4u);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sum += u < S ? part[u] : 0.f;  // S <= 8 (plan)
       ssq[tid] = sum;
     }
     if (tid == 0)
@@ -247,7 +450,7 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
 #pragma unroll
     for (int i = 0; i < 4; ++i) red[t * 16 + 4 * grp + i][col] = acc[t][i];
   __syncthreads();
-  if (tvalid) tile_epilogue<T, EPI, MT>(p, tile, red, inv_rms, norm, lane, 64);
+  if (tvalid) row_epilogue<T, EPI, MT>(p, tile, red, inv_rms, norm, lane);
   if (p.wg_trace != nullptr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -261,15 +464,42 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
   }
 }
 
+// RMSNorm fold per epilogue as the engine uses them: never for the plain / residual
+// projections (x is already the attention / SiLU output), always for qkv and gate_up (eps > 0),
+// either way for the LM-head sampler (decode: final norm fused; prefill rows: already normed)
 template <typename T, int WAVES, int MT>
 static int launch_epi(int epi, dim3 grid, hipStream_t st, const SkinnyParams& p, int ntiles) {
   const dim3 blk(WAVES * 64);
+  const bool norm = p.eps > 0.f;
+  // 6 / 7 waves at 128 rows with the norm fold spill past 256 VGPRs (the plan avoids them)
+  constexpr bool kNormOk = !(MT == 8 && (WAVES == 6 || WAVES == 7));
+  if constexpr (!kNormOk) {
+    if (norm) return -1;
+  }
   switch (epi) {
-    case EPI_PLAIN: wide_kernel<T, WAVES, MT, EPI_PLAIN><<<grid, blk, 0, st>>>(p, ntiles); return 0;
-    case EPI_RESADD: wide_kernel<T, WAVES, MT, EPI_RESADD><<<grid, blk, 0, st>>>(p, ntiles); return 0;
-    case EPI_QKVROPE: wide_kernel<T, WAVES, MT, EPI_QKVROPE><<<grid, blk, 0, st>>>(p, ntiles); return 0;
-    case EPI_SILU: wide_kernel<T, WAVES, MT, EPI_SILU><<<grid, blk, 0, st>>>(p, ntiles); return 0;
-    case EPI_SAMPLE: wide_kernel<T, WAVES, MT, EPI_SAMPLE><<<grid, blk, 0, st>>>(p, ntiles); return 0;
+    case EPI_PLAIN:
+      if (norm) return -1;
+      wide_kernel<T, WAVES, MT, EPI_PLAIN, false><<<grid, blk, 0, st>>>(p, ntiles);
+      return 0;
+    case EPI_RESADD:
+      if (norm) return -1;
+      wide_kernel<T, WAVES, MT, EPI_RESADD, false><<<grid, blk, 0, st>>>(p, ntiles);
+      return 0;
+    case EPI_QKVROPE:
+      if (!norm) return -1;
+      if constexpr (kNormOk) wide_kernel<T, WAVES, MT, EPI_QKVROPE, true><<<grid, blk, 0, st>>>(p, ntiles);
+      return 0;
+    case EPI_SILU:
+      if (!norm) return -1;
+      if constexpr (kNormOk) wide_kernel<T, WAVES, MT, EPI_SILU, true><<<grid, blk, 0, st>>>(p, ntiles);
+      return 0;
+    case EPI_SAMPLE:
+      if (norm) {
+        if constexpr (kNormOk) wide_kernel<T, WAVES, MT, EPI_SAMPLE, true><<<grid, blk, 0, st>>>(p, ntiles);
+      } else {
+        wide_kernel<T, WAVES, MT, EPI_SAMPLE, false><<<grid, blk, 0, st>>>(p, ntiles);
+      }
+      return 0;
     default: return -1;
   }
 }
@@ -303,7 +533,7 @@ static int launch_mt(int epi, int mt, int waves, dim3 grid, hipStream_t st,
 // per-CU streaming rate, plus ~1.5 us of ramp), plus the split-K hand-over (~1 us + 0.4 us
 // per slice the last arriver reads back) - and the cheapest wins.  Slices keep >= 2 chunks
 // of K.
-static void plan(int ntiles, int K, int M, int& waves, int& ksplit) {
+static void plan(int ntiles, int K, int M, bool norm, int& waves, int& ksplit) {
   constexpr double kCUs = 256.0, kBpus = 24e3;  // bytes per us per CU
   const int mpad = ((M + 15) / 16) * 16;
   const int nch = K / kKC;
@@ -311,6 +541,7 @@ static void plan(int ntiles, int K, int M, int& waves, int& ksplit) {
   const int ws[4] = {4, 6, 7, 8};
   for (int wi = 0; wi < 4; ++wi) {
     const int w = ws[wi];
+    if (norm && M > 96 && (w == 6 || w == 7)) continue;  // see launch_epi
     const int ncb = (ntiles + w - 1) / w;
     for (int s = 1; s <= 8 && nch / s >= 2; ++s) {
       const double rounds = std::ceil(ncb * s / kCUs);
@@ -341,7 +572,7 @@ int atta_wide_launch(SkinnyParams& p, int epi, int ntiles, int waves, int ksplit
                      const float* sk_ws, int* sk_counters, int64_t ws_floats, int n_counters,
                      hipStream_t stream) {
   if (p.M < 1 || p.M > 128 || p.K % wide::kKC != 0 || !p.ps || p.wscale != nullptr) return -1;
-  if (waves <= 0 || ksplit <= 0) wide::plan(ntiles, p.K, p.M, waves, ksplit);
+  if (waves <= 0 || ksplit <= 0) wide::plan(ntiles, p.K, p.M, p.eps > 0.f, waves, ksplit);
   if (waves != 4 && waves != 6 && waves != 7 && waves != 8) return -1;
   if (ksplit < 1 || p.K / wide::kKC < ksplit) return -1;
   const int mt = p.M <= 32 ? 2 : p.M <= 64 ? 4 : p.M <= 96 ? 6 : 8;

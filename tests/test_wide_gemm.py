@@ -67,6 +67,8 @@ def test_wide_linear_plain_and_residual(plan, m, n, k):
 @pytest.mark.parametrize("m", [33, 85, 128])
 @pytest.mark.parametrize("hq,hkv,H", [(32, 8, 4096), (8, 1, 8192)])
 def test_wide_qkv_rope(plan, m, hq, hkv, H):
+    if m > 96 and plan[0] in (6, 7):
+        pytest.skip("6 / 7 waves x 128 rows with the norm fold is not built (VGPR spill)")
     torch.manual_seed(42)
     dt, bs, nb = torch.bfloat16, 16, 64
     x = torch.randn(m, H, dtype=dt, device="cuda") * 2
@@ -92,6 +94,8 @@ def test_wide_qkv_rope(plan, m, hq, hkv, H):
 @pytest.mark.parametrize("m", [40, 85, 128])
 @pytest.mark.parametrize("inter,k", [(14336, 4096), (1792, 8192)])
 def test_wide_gate_up_silu(plan, m, inter, k):
+    if m > 96 and plan[0] in (6, 7):
+        pytest.skip("6 / 7 waves x 128 rows with the norm fold is not built (VGPR spill)")
     torch.manual_seed(43)
     dt = torch.bfloat16
     x = torch.randn(m, k, dtype=dt, device="cuda")
