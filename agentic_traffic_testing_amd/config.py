@@ -183,6 +183,10 @@ def _env_int(name, default):
 class EngineConfig:
     model: str = "meta-llama/Llama-3.1-8B-Instruct"
     dtype: str = "bfloat16"              # reference default float16; both supported
+    # Limit: the flash prefill kernel stages a sequence's whole block-table row in LDS (2048
+    # entries = 32k tokens at block_size 16).  max_model_len beyond that sends EVERY prefill
+    # to the slower v1 kernel (ops.prefill_impl picks by table width, not by the batch) -
+    # raise block_size with it (block_size 32 keeps flash up to 64k).
     max_model_len: int = 4096
     max_num_seqs: int = 12
     max_num_batched_tokens: int = 8192
@@ -209,6 +213,10 @@ class EngineConfig:
     # context, not max_model_len); buckets above max_model_len's count are dropped
     graph_parts_buckets: tuple = (1, 2, 4, 6, 8, 12, 16, 24, 32, 48, 64)
     decode_small_batch_max: int = 8
+    # finest tier: B <= decode_tiny_batch_max (the fan-out's planning / synthesis decode, B = 1)
+    # splits into 64-token partitions (0 = off)
+    decode_partition_tokens_tiny: int = 64
+    decode_tiny_batch_max: int = 2
     # chunked prefill: max prompt tokens of one sequence per step (0 = max_num_batched_tokens)
     long_prefill_token_threshold: int = 0
     # fused native decode path (GEMV kernels) when available

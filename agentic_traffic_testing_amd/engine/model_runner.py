@@ -146,12 +146,21 @@ class ModelRunner:
         self.part_tokens = cfg.decode_partition_tokens
         self.max_parts = max(1, math.ceil(cfg.max_model_len / self.part_tokens))
         # small decode batches split the context finer (more workgroups in flight for the
-        # latency-bound B<=2 attention); partial buffers are sized for the finest split
-        self.part_tokens_small = cfg.decode_partition_tokens_small or self.part_tokens
-        self.max_parts_small = max(1, math.ceil(cfg.max_model_len / self.part_tokens_small))
-        if self.max_parts_small > 64:  # in-kernel combine handles <= 64 partitions
-            self.part_tokens_small, self.max_parts_small = self.part_tokens, self.max_parts
-        alloc_parts = max(self.max_parts, self.max_parts_small)
+        # latency-bound attention): partition tiers by batch size, finest first - tiny
+        # (<= decode_tiny_batch_max, 64 tokens: B = 1 at 0.6-3.5k context 7.3 / 8.8 us vs 8.4 /
+        # 10.7 at 128, profiles/r5_attention_partitions.txt) and small (<=
+        # decode_small_batch_max, 128 tokens); partial buffers are sized for the finest split
+        self.part_tiers = []  # (max batch, partition tokens, max partitions, graph buckets)
+        for mb, pt in ((cfg.decode_tiny_batch_max, cfg.decode_partition_tokens_tiny),
+                       (cfg.decode_small_batch_max, cfg.decode_partition_tokens_small)):
+            if mb <= 0 or not pt or pt == self.part_tokens:
+                continue
+            mp = max(1, math.ceil(cfg.max_model_len / pt))
+            if mp > 64:  # in-kernel combine handles <= 64 partitions
+                continue
+            bk = sorted({p for p in cfg.graph_parts_buckets if p < mp} | {mp})
+            self.part_tiers.append((mb, pt, mp, bk))
+        alloc_parts = max([self.max_parts] + [t[2] for t in self.part_tiers])
         # decode graphs are captured per (batch bucket, partition bucket): the attention grid
         # is (seqs, kv heads, partitions) and every workgroup past a sequence's context still
         # costs a dispatch and a round trip - a 32-partition grid (max_model_len 8192) over
@@ -159,9 +168,6 @@ class ModelRunner:
         # (profiles/r2_fused_qkv_attn_experiment.txt: B=8 attention 21.9 us vs 10.8 at B=1)
         self.parts_buckets = sorted({p for p in cfg.graph_parts_buckets if p < self.max_parts}
                                     | {self.max_parts})
-        self.parts_buckets_small = sorted(
-            {p for p in cfg.graph_parts_buckets if p < self.max_parts_small}
-            | {self.max_parts_small})
         self.tile_tokens = ops.prefill_tile_tokens(self.model.g, bt_width=self.bt_width)
         self.graph_sizes = sorted(b for b in cfg.graph_batch_sizes)
         cap = next((b for b in self.graph_sizes if b >= cfg.max_num_seqs), cfg.max_num_seqs)
@@ -298,11 +304,19 @@ class ModelRunner:
         return self.num_blocks * self.block_size
 
     # ------------------------------------------------------------------------------------
+    def _tier(self, batch_size: int) -> tuple:
+        """(partition tokens, max partitions, graph partition buckets) of a decode step of
+        ``batch_size`` rows (the graph bucket when replayed)."""
+        for mb, pt, mp, bk in self.part_tiers:
+            if 0 < batch_size <= mb:
+                return pt, mp, bk
+        return self.part_tokens, self.max_parts, self.parts_buckets
+
     def _ws_for(self, batch_size: int) -> dict:
-        if self._small(batch_size):
-            return {**self.ws, "part_tokens": self.part_tokens_small,
-                    "max_parts": self.max_parts_small}
-        return self.ws
+        pt, mp, _ = self._tier(batch_size)
+        if pt == self.part_tokens:
+            return self.ws
+        return {**self.ws, "part_tokens": pt, "max_parts": mp}
 
     def _prepare(self, batch: Batch, pad_seqs: int = 0, tiles: bool = True):
         ids, qs, ql = batch.arrays()
@@ -378,17 +392,10 @@ class ModelRunner:
                         tile_qoff=v["tile_qoff"], logits_idx=v["logits_idx"],
                         num_decode=num_decode, num_tiles=num_tiles)
 
-    def _small(self, batch_size: int) -> bool:
-        return (0 < batch_size <= self.cfg.decode_small_batch_max
-                and self.part_tokens_small != self.part_tokens)
-
     def parts_bucket(self, max_kv: int, batch_size: int = 0) -> int:
         """Smallest partition bucket covering a decode step of ``batch_size`` rows whose
         longest context is max_kv (in the partition size that batch size uses)."""
-        if self._small(batch_size):
-            pt, buckets, top = self.part_tokens_small, self.parts_buckets_small, self.max_parts_small
-        else:
-            pt, buckets, top = self.part_tokens, self.parts_buckets, self.max_parts
+        pt, top, buckets = self._tier(batch_size)
         need = max(1, math.ceil(max_kv / pt))
         return next((p for p in buckets if p >= need), top)
 
@@ -646,7 +653,7 @@ class ModelRunner:
         """Capture a decode step for `bucket` sequences whose contexts fit `parts` attention
         partitions (default: max_model_len) into a hipGraph; ``special``: the top-k / top-p
         sampler variant (logits materialised)."""
-        parts = parts or (self.max_parts_small if self._small(bucket) else self.max_parts)
+        parts = parts or self._tier(bucket)[1]
         if self.publisher is not None:
             hdr = np.zeros(HDR_WORDS, dtype=np.int32)
             hdr[0], hdr[1], hdr[2], hdr[3] = OP_CAPTURE, bucket, parts, int(special)
@@ -702,9 +709,7 @@ class ModelRunner:
         for b in self.graph_sizes:
             if not self._graph_ok(b):
                 continue
-            small = self._small(b)
-            top = self.max_parts_small if small else self.max_parts
-            buckets = self.parts_buckets_small if small else self.parts_buckets
+            _, top, buckets = self._tier(b)
             for p in (buckets if all_parts else [top]):
                 if (b, p, 0) not in self.graphs:
                     self.capture(b, p)

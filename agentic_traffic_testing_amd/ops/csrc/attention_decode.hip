@@ -384,11 +384,12 @@ static int launch_g(int G, dim3 grid, hipStream_t st, const DecParams& p) {
   }
 }
 
-// part_tokens selects the workgroup shape: 128 = 4 waves x 2 tiles, 256 = 8 x 2,
-// 512 = 16 x 2 (16 waves cap VGPRs at 128: more tiles per wave would spill).
+// part_tokens selects the workgroup shape: 64 = 4 waves x 1 tile, 128 = 4 waves x 2 tiles,
+// 256 = 8 x 2, 512 = 16 x 2 (16 waves cap VGPRs at 128: more tiles per wave would spill).
 template <typename T>
 static int launch(int G, int part_tokens, dim3 grid, hipStream_t st, const DecParams& p) {
   switch (part_tokens) {
+    case 64: return launch_g<T, 4, 1>(G, grid, st, p);
     case 128: return launch_g<T, 4, 2>(G, grid, st, p);
     case 256: return launch_g<T, 8, 2>(G, grid, st, p);
     case 512: return launch_g<T, 16, 2>(G, grid, st, p);

@@ -38,17 +38,8 @@ template <typename T, int WAVES, int UNROLL, int MT, int EPI, bool NTL = false, 
 __global__ __launch_bounds__(WAVES * 64) void skinny_kernel(SkinnyParams p) {
   unsigned long long t0 = 0;
   if (p.wg_trace != nullptr) t0 = wall_clock64();
-  int tile = blockIdx.x, ks = blockIdx.y, ksplit = p.ksplit;
-  if (p.split_from > 0) {  // tail split: tiles >= split_from run ksplit ways along x
-    const int b = blockIdx.x - p.split_from;
-    if (b < 0) {
-      ksplit = 1;
-    } else {
-      tile = p.split_from + b / p.ksplit;
-      ks = b % p.ksplit;
-    }
-  }
-  skinny_body<T, WAVES, UNROLL, MT, EPI, NTL, PS, W8>(p, tile, ks, ksplit);
+  const int tile = blockIdx.x, ks = blockIdx.y;
+  skinny_body<T, WAVES, UNROLL, MT, EPI, NTL, PS, W8>(p, tile, ks, p.ksplit);
   if (p.wg_trace != nullptr && ks == 0) {  // timeline probe (one entry per tile, bounded by
     // the tile count whatever the split): every thread's stores issued, then one stamp
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -250,43 +241,8 @@ static int wide(SkinnyParams& p, int epi, int ntiles, int dtype, hipStream_t str
 // Resolve the split for one launch: waves fitted to the K slice (fp8: 64-wide granule), the
 // split reduced until every wave's slice is whole; a split > 1 needs the device workspace.
 // Returns 0 or -1 (unsupported), -2 (split requested but no / too small workspace).
-// Tail split (SkinnyParams.split_from): with no split requested, a grid of 1.25-1.75 rounds of
-// tiles over the CUs runs its partial round's tiles 2 ways, so every CU streams ~the same
-// bytes (qkv: 256 whole tiles + 128 tiles x 2 halves; was 2 tiles on half the CUs, 1 on the
-// rest).  ATTA_TAIL_SPLIT=0 turns it off.
-static int tail_split_on() {
-  static const int on = [] {
-    const char* e = std::getenv("ATTA_TAIL_SPLIT");
-    return e == nullptr ? 1 : (e[0] == '1' ? 1 : 0);
-  }();
-  return on;
-}
-constexpr int kCUs = 256;
-static dim3 split_grid(const SkinnyParams& p, int tiles) {
-  if (p.split_from > 0) return dim3(p.split_from + (tiles - p.split_from) * p.ksplit, 1);
-  return dim3(tiles, p.ksplit);
-}
-
 static int setup_split(SkinnyParams& p, int& waves, int ksplit, int tiles, bool fp8) {
   const int gran = fp8 ? 64 : 32;
-  p.split_from = 0;
-  if (ksplit == 1 && tail_split_on() && tiles > kCUs) {
-    const int rem = tiles % kCUs;
-    if (rem >= kCUs / 4 && rem <= 3 * kCUs / 4 &&
-        p.K % (2 * gran * fit_waves(waves, p.K / 2, fp8)) == 0) {
-      int dev = 0;
-      if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 &&
-          g_splitk[dev].ws != nullptr && tiles <= g_splitk[dev].n_counters &&
-          static_cast<int64_t>(tiles) * 2 * (p.M <= 16 ? 16 : 32) * 17 <= g_splitk[dev].ws_floats) {
-        waves = fit_waves(waves, p.K / 2, fp8);
-        p.ksplit = 2;
-        p.split_from = tiles - rem;
-        p.sk_ws = g_splitk[dev].ws;
-        p.sk_counters = g_splitk[dev].counters;
-        return 0;
-      }
-    }
-  }
   if (ksplit < 1) ksplit = 1;
   while (ksplit > 1 && p.K % (ksplit * gran * 4) != 0) ksplit >>= 1;
   waves = fit_waves(waves, p.K / ksplit, fp8);
@@ -329,7 +285,7 @@ int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual
   }
   if (const int rc = setup_split(p, waves, ksplit, N / 16, wscale != nullptr)) return rc;
   const int mt = M <= 16 ? 1 : 2;
-  dim3 grid = split_grid(p, N / 16);
+  dim3 grid(N / 16, p.ksplit);
   p.wg_trace = take_trace();
   if (residual != nullptr) {
     // y := residual + x W^T, computed in place on the residual buffer when y == residual;
@@ -375,7 +331,7 @@ int atta_skinny_gemm_push(const void* x, const void* w, int M, int N, int K, int
   p.push_max_elems = max_elems;
   if (const int rc = setup_split(p, waves, ksplit, N / 16, wscale != nullptr)) return rc;
   const int mt = M <= 16 ? 1 : 2;
-  dim3 grid = split_grid(p, N / 16);
+  dim3 grid(N / 16, p.ksplit);
   p.wg_trace = take_trace();
   launch_epi<EPI_PLAIN>(dtype, mt, waves, grid, stream, p);
   return static_cast<int>(hipGetLastError());
@@ -414,7 +370,7 @@ int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x
   p.bs_shift = shift;
   if (use_wide(M)) return wide(p, EPI_QKVROPE, p.N / 16, dtype, stream);
   if (const int rc = setup_split(p, waves, ksplit, p.N / 16, wscale != nullptr)) return rc;
-  dim3 grid = split_grid(p, p.N / 16);
+  dim3 grid(p.N / 16, p.ksplit);
   p.wg_trace = take_trace();
   launch_epi<EPI_QKVROPE>(dtype, M <= 16 ? 1 : 2, waves, grid, stream, p);
   return static_cast<int>(hipGetLastError());
@@ -441,7 +397,7 @@ int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int 
   p.eps = eps;
   if (use_wide(M)) return wide(p, EPI_SILU, inter / 8, dtype, stream);
   if (const int rc = setup_split(p, waves, ksplit, inter / 8, wscale != nullptr)) return rc;
-  dim3 grid = split_grid(p, inter / 8);
+  dim3 grid(inter / 8, p.ksplit);
   p.wg_trace = take_trace();
   launch_epi<EPI_SILU>(dtype, M <= 16 ? 1 : 2, waves, grid, stream, p);
   return static_cast<int>(hipGetLastError());

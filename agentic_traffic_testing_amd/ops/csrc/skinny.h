@@ -91,11 +91,6 @@ struct SkinnyParams {
   int ksplit;
   float* sk_ws;
   int* sk_counters;
-  // tail split (gridDim.y == 1): tiles below split_from run unsplit, the remaining tiles
-  // ksplit ways - a grid of tiles that is not a multiple of the CU count (qkv: 384 tiles on
-  // 256 CUs) gets its last partial round spread over every CU instead of doubling half of
-  // them.  0 = off (every tile split ksplit ways along gridDim.y)
-  int split_from;
   // optional per-workgroup timeline (ops.set_gemv_trace): [start, end] on the 100 MHz wall
   // clock per workgroup of the grid (gridDim.y == 1 launches only)
   unsigned long long* wg_trace;

@@ -39,60 +39,107 @@ constexpr int kKC = 128;             // K columns per staged chunk (4 MFMA K ste
 constexpr int kRowB = kKC * 2;       // bytes of one staged x row
 constexpr int kSlots = kRowB / 16;   // 16-B slots per staged row
 
-// Epilogue of one wave's 16-column tile, one accumulator ROW per lane (rows lane and lane + 64):
-// every global load of a row (residual segment, position / slot / cos-sin, sampler params) is
-// issued before any of its uses and rows move as 16-B vectors.  (The element-per-thread
-// tile_epilogue of the GEMV, run by one wave over up to 128 rows, paid one dependent load
-// round trip per element: 24 serialized residual loads per wave at 96 rows.)
-template <typename T, int EPI, int MT>
-__device__ __forceinline__ void row_epilogue(const SkinnyParams& p, const int tile,
-                                             const float (*red)[17], const float* inv_rms,
-                                             const bool norm, const int lane) {
-  constexpr int RPL = MT * 16 > 64 ? 2 : 1;  // rows per lane
+// Epilogue of one wave's 16-column tile, one accumulator ROW per lane (rows lane and lane + 64),
+// in two phases: epi_load issues every global load the epilogue needs (residual segment,
+// position / slot then cos-sin, sampler parameters) as early as the kernel can - before the
+// split-K arrival counter, so they overlap the hand-over - and epi_apply computes and stores
+// 16-B row vectors.  (The GEMV's element-per-thread tile_epilogue, run by one wave over up to
+// 128 rows, paid one dependent load round trip per element: 24 per wave at 96 rows.)
+template <int MT>
+struct EpiIn {
+  static constexpr int RPL = MT * 16 > 64 ? 2 : 1;  // rows per lane
   int rows[RPL];
   bool ok[RPL];
+  u32x4 res[RPL][2];  // RESADD: the residual row segment (16 values)
+  int slot[RPL];      // QKVROPE
+  f32x4 cs[RPL][4];   // QKVROPE: cos d..d+7, sin d..d+7
+  float temp[RPL];    // SAMPLE
+  uint64_t seed[RPL], step[RPL];
+};
+
+template <typename T, int EPI, int MT>
+__device__ __forceinline__ void epi_load(const SkinnyParams& p, const int tile, const int lane,
+                                         EpiIn<MT>& in) {
+  constexpr int RPL = EpiIn<MT>::RPL;
 #pragma unroll
   for (int j = 0; j < RPL; ++j) {
-    rows[j] = lane + 64 * j;
-    ok[j] = rows[j] < MT * 16 && rows[j] < p.M;
+    in.rows[j] = lane + 64 * j;
+    in.ok[j] = in.rows[j] < MT * 16 && in.rows[j] < p.M;
   }
-  if constexpr (EPI == EPI_PLAIN || EPI == EPI_RESADD) {
-    u32x4 res[RPL][2];
-    if constexpr (EPI == EPI_RESADD) {
-#pragma unroll
-      for (int j = 0; j < RPL; ++j) {
-        const u32x4* src = reinterpret_cast<const u32x4*>(
-            p.y + static_cast<int64_t>(ok[j] ? rows[j] : 0) * p.y_stride + tile * 16);
-        res[j][0] = src[0];
-        res[j][1] = src[1];
-      }
-    }
+  if constexpr (EPI == EPI_RESADD) {
 #pragma unroll
     for (int j = 0; j < RPL; ++j) {
-      if (!ok[j]) continue;
-      const int m = rows[j];
+      const u32x4* src = reinterpret_cast<const u32x4*>(
+          p.y + static_cast<int64_t>(in.ok[j] ? in.rows[j] : 0) * p.y_stride + tile * 16);
+      in.res[j][0] = src[0];
+      in.res[j][1] = src[1];
+    }
+  } else if constexpr (EPI == EPI_QKVROPE) {
+    const int head = tile >> 3, jb = (tile & 7) * 8;
+    int pos[RPL];
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      const int m = in.ok[j] ? in.rows[j] : 0;
+      pos[j] = p.positions[m];
+      in.slot[j] = p.slots[m];
+    }
+    if (head < p.n_q_heads + p.n_kv_heads) {
+#pragma unroll
+      for (int j = 0; j < RPL; ++j) {
+        const f32x4* c4 =
+            reinterpret_cast<const f32x4*>(p.cos_sin + static_cast<int64_t>(pos[j]) * 128 + jb);
+        in.cs[j][0] = c4[0];
+        in.cs[j][1] = c4[1];
+        in.cs[j][2] = c4[16];  // + 64 floats: the sin half
+        in.cs[j][3] = c4[17];
+      }
+    }
+  } else if constexpr (EPI == EPI_SAMPLE) {
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      const int m = in.ok[j] ? in.rows[j] : 0;
+      in.temp[j] = p.temperature[m];
+      in.seed[j] = static_cast<uint64_t>(p.seeds[m]);
+      in.step[j] = static_cast<uint64_t>(p.steps[m]);
+    }
+  }
+}
+
+__device__ __forceinline__ u32x4 pack8(const uint16_t (&o)[8]) {
+  return u32x4{o[0] | (uint32_t(o[1]) << 16), o[2] | (uint32_t(o[3]) << 16),
+               o[4] | (uint32_t(o[5]) << 16), o[6] | (uint32_t(o[7]) << 16)};
+}
+
+template <typename T, int EPI, int MT>
+__device__ __forceinline__ void epi_apply(const SkinnyParams& p, const int tile,
+                                          const float (*red)[17], const float* inv_rms,
+                                          const bool norm, const EpiIn<MT>& in) {
+  constexpr int RPL = EpiIn<MT>::RPL;
+  if constexpr (EPI == EPI_PLAIN || EPI == EPI_RESADD) {
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      if (!in.ok[j]) continue;
+      const int m = in.rows[j];
       const float sc = norm ? inv_rms[m] : 1.f;
-      uint16_t o[16];
+      uint16_t o[2][8];
 #pragma unroll
       for (int n = 0; n < 16; ++n) {
         float v = red[m][n] * sc;
         if constexpr (EPI == EPI_RESADD) {
-          const uint32_t w = res[j][n >> 3][(n >> 1) & 3];
+          const uint32_t w = in.res[j][n >> 3][(n >> 1) & 3];
           v = to_f32<T>(from_f32<T>(v)) + to_f32<T>(static_cast<uint16_t>((n & 1) ? w >> 16 : w));
         }
-        o[n] = from_f32<T>(v);
+        o[n >> 3][n & 7] = from_f32<T>(v);
       }
       u32x4* dst = reinterpret_cast<u32x4*>(p.y + static_cast<int64_t>(m) * p.y_stride + tile * 16);
-      dst[0] = u32x4{o[0] | (uint32_t(o[1]) << 16), o[2] | (uint32_t(o[3]) << 16),
-                     o[4] | (uint32_t(o[5]) << 16), o[6] | (uint32_t(o[7]) << 16)};
-      dst[1] = u32x4{o[8] | (uint32_t(o[9]) << 16), o[10] | (uint32_t(o[11]) << 16),
-                     o[12] | (uint32_t(o[13]) << 16), o[14] | (uint32_t(o[15]) << 16)};
+      dst[0] = pack8(o[0]);
+      dst[1] = pack8(o[1]);
     }
   } else if constexpr (EPI == EPI_SILU) {
 #pragma unroll
     for (int j = 0; j < RPL; ++j) {
-      if (!ok[j]) continue;
-      const int m = rows[j];
+      if (!in.ok[j]) continue;
+      const int m = in.rows[j];
       const float sc = norm ? inv_rms[m] : 1.f;
       uint16_t o[8];
 #pragma unroll
@@ -102,36 +149,16 @@ __device__ __forceinline__ void row_epilogue(const SkinnyParams& p, const int ti
         const float si = to_f32<T>(from_f32<T>(g / (1.f + __expf(-g))));
         o[c] = from_f32<T>(si * u);
       }
-      *reinterpret_cast<u32x4*>(p.y + static_cast<int64_t>(m) * p.y_stride + tile * 8) =
-          u32x4{o[0] | (uint32_t(o[1]) << 16), o[2] | (uint32_t(o[3]) << 16),
-                o[4] | (uint32_t(o[5]) << 16), o[6] | (uint32_t(o[7]) << 16)};
+      *reinterpret_cast<u32x4*>(p.y + static_cast<int64_t>(m) * p.y_stride + tile * 8) = pack8(o);
     }
   } else if constexpr (EPI == EPI_QKVROPE) {
     const int head = tile >> 3, jb = (tile & 7) * 8;
     const int nq = p.n_q_heads, nkv = p.n_kv_heads;
     const int BS = 1 << p.bs_shift;
-    int pos[RPL], slot[RPL];
 #pragma unroll
     for (int j = 0; j < RPL; ++j) {
-      const int m = ok[j] ? rows[j] : 0;
-      pos[j] = p.positions[m];
-      slot[j] = p.slots[m];
-    }
-    f32x4 cs[RPL][4];  // cos d..d+7, sin d..d+7
-    if (head < nq + nkv) {
-#pragma unroll
-      for (int j = 0; j < RPL; ++j) {
-        const f32x4* c4 = reinterpret_cast<const f32x4*>(p.cos_sin + static_cast<int64_t>(pos[j]) * 128 + jb);
-        cs[j][0] = c4[0];
-        cs[j][1] = c4[1];
-        cs[j][2] = c4[16];  // + 64 floats
-        cs[j][3] = c4[17];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < RPL; ++j) {
-      if (!ok[j]) continue;
-      const int m = rows[j];
+      if (!in.ok[j]) continue;
+      const int m = in.rows[j];
       const float sc = norm ? inv_rms[m] : 1.f;
       uint16_t o1[8], o2[8];
 #pragma unroll
@@ -140,7 +167,7 @@ __device__ __forceinline__ void row_epilogue(const SkinnyParams& p, const int ti
         const float x1 = to_f32<T>(from_f32<T>(red[m][c] * sc));
         const float x2 = to_f32<T>(from_f32<T>(red[m][c + 8] * sc));
         if (head < nq + nkv) {
-          const float co = cs[j][c >> 2][c & 3], si = cs[j][2 + (c >> 2)][c & 3];
+          const float co = in.cs[j][c >> 2][c & 3], si = in.cs[j][2 + (c >> 2)][c & 3];
           o1[c] = from_f32<T>(x1 * co - x2 * si);
           o2[c] = from_f32<T>(x2 * co + x1 * si);
         } else {
@@ -148,54 +175,39 @@ __device__ __forceinline__ void row_epilogue(const SkinnyParams& p, const int ti
           o2[c] = from_f32<T>(x2);
         }
       }
-      const u32x4 v1 = {o1[0] | (uint32_t(o1[1]) << 16), o1[2] | (uint32_t(o1[3]) << 16),
-                        o1[4] | (uint32_t(o1[5]) << 16), o1[6] | (uint32_t(o1[7]) << 16)};
-      const u32x4 v2 = {o2[0] | (uint32_t(o2[1]) << 16), o2[2] | (uint32_t(o2[3]) << 16),
-                        o2[4] | (uint32_t(o2[5]) << 16), o2[6] | (uint32_t(o2[7]) << 16)};
+      const int sl = in.slot[j];
       if (head < nq) {
         uint16_t* q = p.y + static_cast<int64_t>(m) * p.y_stride + head * 128 + jb;
-        *reinterpret_cast<u32x4*>(q) = v1;
-        *reinterpret_cast<u32x4*>(q + 64) = v2;
-      } else if (slot[j] >= 0) {
-        const int sl = slot[j];
-        if (head < nq + nkv) {
-          uint16_t* kc = p.k_cache + ((static_cast<int64_t>(sl >> p.bs_shift) * nkv + (head - nq)) * BS +
-                                      (sl & (BS - 1))) * 128 + jb;
-          *reinterpret_cast<u32x4*>(kc) = v1;
-          *reinterpret_cast<u32x4*>(kc + 64) = v2;
-        } else {
-          uint16_t* vc = p.v_cache + (static_cast<int64_t>(sl >> p.bs_shift) * nkv + (head - nq - nkv)) *
-                                         128 * BS + (sl & (BS - 1));
+        *reinterpret_cast<u32x4*>(q) = pack8(o1);
+        *reinterpret_cast<u32x4*>(q + 64) = pack8(o2);
+      } else if (sl >= 0 && head < nq + nkv) {
+        uint16_t* kc = p.k_cache + ((static_cast<int64_t>(sl >> p.bs_shift) * nkv + (head - nq)) * BS +
+                                    (sl & (BS - 1))) * 128 + jb;
+        *reinterpret_cast<u32x4*>(kc) = pack8(o1);
+        *reinterpret_cast<u32x4*>(kc + 64) = pack8(o2);
+      } else if (sl >= 0) {
+        uint16_t* vc = p.v_cache + (static_cast<int64_t>(sl >> p.bs_shift) * nkv + (head - nq - nkv)) *
+                                       128 * BS + (sl & (BS - 1));
 #pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            vc[static_cast<int64_t>(jb + c) * BS] = o1[c];
-            vc[static_cast<int64_t>(jb + c + 64) * BS] = o2[c];
-          }
+        for (int c = 0; c < 8; ++c) {
+          vc[static_cast<int64_t>(jb + c) * BS] = o1[c];
+          vc[static_cast<int64_t>(jb + c + 64) * BS] = o2[c];
         }
       }
     }
   } else if constexpr (EPI == EPI_SAMPLE) {
-    float temp[RPL];
-    uint64_t seed[RPL], step[RPL];
 #pragma unroll
     for (int j = 0; j < RPL; ++j) {
-      const int m = ok[j] ? rows[j] : 0;
-      temp[j] = p.temperature[m];
-      seed[j] = static_cast<uint64_t>(p.seeds[m]);
-      step[j] = static_cast<uint64_t>(p.steps[m]);
-    }
-#pragma unroll
-    for (int j = 0; j < RPL; ++j) {
-      if (!ok[j]) continue;
-      const int m = rows[j];
+      if (!in.ok[j]) continue;
+      const int m = in.rows[j];
       const float sc = norm ? inv_rms[m] : 1.f;
       unsigned long long best = 0ull;
 #pragma unroll
       for (int n = 0; n < 16; ++n) {
         float v = to_f32<T>(from_f32<T>(red[m][n] * sc));  // bf16 logits, as F.linear
         const int idx = p.vocab_offset + tile * 16 + n;    // global id: TP == TP1 noise
-        if (temp[j] > 1e-5f)
-          v = v / temp[j] + gumbel_noise(seed[j], step[j], static_cast<uint32_t>(idx));
+        if (in.temp[j] > 1e-5f)
+          v = v / in.temp[j] + gumbel_noise(in.seed[j], in.step[j], static_cast<uint32_t>(idx));
         const unsigned long long key =
             (static_cast<unsigned long long>(ordered_bits(v)) << 32) |
             static_cast<unsigned long long>(0xFFFFFFFFu - static_cast<unsigned>(idx));
@@ -376,6 +388,9 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
     }
   }
   __syncthreads();  // x buffers free from here on (the epilogue tiles reuse them)
+  // the epilogue's global inputs, in flight across the hand-over below
+  EpiIn<MT> ein;
+  epi_load<T, EPI, MT>(p, tvalid ? tile : 0, lane, ein);
 
   if (S > 1) {
     // ---- split-K hand-over: device-scope stores + arrival counter (common.h) -------------
@@ -410,9 +425,9 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
     }
     const uint32_t first = static_cast<uint32_t>(cb * S) * per_slice +
                            static_cast<uint32_t>(wid * R * 16 + col * R + 4 * grp);
-    // QB slices' partials in flight per round trip (<= 16 16-B loads per lane), summed in
-    // slice order: deterministic
-    constexpr int QB = MT <= 2 ? 8 : MT <= 4 ? 4 : 2;
+    // QB slices' partials in flight per round trip (<= 32 16-B loads per lane: S <= 4 at 128
+    // rows, S <= 8 below 80 - one round trip), summed in slice order: deterministic
+    constexpr int QB = MT <= 4 ? 8 : MT <= 6 ? 5 : 4;
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int q0 = 0; q0 < S; q0 += QB) {
@@ -450,7 +465,7 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
 #pragma unroll
     for (int i = 0; i < 4; ++i) red[t * 16 + 4 * grp + i][col] = acc[t][i];
   __syncthreads();
-  if (tvalid) row_epilogue<T, EPI, MT>(p, tile, red, inv_rms, norm, lane);
+  if (tvalid) epi_apply<T, EPI, MT>(p, tile, red, inv_rms, norm, ein);
   if (p.wg_trace != nullptr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

@@ -114,13 +114,21 @@ def test_parts_buckets_cover_context():
     assert r.parts_bucket(1) == 1 and r.parts_bucket(257) == 2 and r.parts_bucket(1025) == 6
     # small decode batches with a finer partition size bucket in their own unit
     cfg = EngineConfig(model="tiny", device="cpu", max_model_len=3000, num_kv_blocks=64,
-                       decode_partition_tokens_small=128, decode_small_batch_max=2)
+                       decode_partition_tokens_small=128, decode_small_batch_max=2,
+                       decode_tiny_batch_max=0)
     r = LLMEngine(cfg).runner
-    assert r.max_parts_small == 24 and r.parts_buckets_small[-1] == 24
+    assert r._tier(2)[1] == 24 and r._tier(2)[2][-1] == 24
     assert r.parts_bucket(1025, 1) == 12 and r.parts_bucket(1025, 2) == 12
     assert r.parts_bucket(1025, 4) == 6
     for kv in range(1, 3001, 7):
         assert r.parts_bucket(kv, 1) * 128 >= kv and r.parts_bucket(kv, 3) * 256 >= kv
+    # three tiers (the defaults): 64-token partitions for B <= 2, 128 for B <= 8, 256 above
+    r = LLMEngine(EngineConfig(model="tiny", device="cpu", max_model_len=3000,
+                               num_kv_blocks=64)).runner
+    assert [r._tier(b)[0] for b in (1, 2, 3, 8, 9)] == [64, 64, 128, 128, 256]
+    assert r._tier(1)[1] == 47 and r.parts_bucket(1025, 1) == 24  # ceil(1025 / 64) = 17
+    for kv in range(1, 3001, 7):
+        assert r.parts_bucket(kv, 2) * 64 >= kv and r.parts_bucket(kv, 5) * 128 >= kv
 
 
 @pytest.mark.gpu
