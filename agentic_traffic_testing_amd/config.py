@@ -213,10 +213,12 @@ class EngineConfig:
     # context, not max_model_len); buckets above max_model_len's count are dropped
     graph_parts_buckets: tuple = (1, 2, 4, 6, 8, 12, 16, 24, 32, 48, 64)
     decode_small_batch_max: int = 8
-    # finest tier: B <= decode_tiny_batch_max (the fan-out's planning / synthesis decode, B = 1)
-    # splits into 64-token partitions (0 = off)
+    # optional finest tier: B <= decode_tiny_batch_max splits into 64-token partitions
+    # (0 = off, the default: faster in isolation - B = 1 at 0.6-3.5k context 7.3 / 8.8 us vs
+    # 8.4 / 10.7 at 128 - but it lost in situ, bench 751.9 vs 756.9 tok/s on one box:
+    # profiles/r5_attention_partitions.txt)
     decode_partition_tokens_tiny: int = 64
-    decode_tiny_batch_max: int = 2
+    decode_tiny_batch_max: int = 0
     # chunked prefill: max prompt tokens of one sequence per step (0 = max_num_batched_tokens)
     long_prefill_token_threshold: int = 0
     # fused native decode path (GEMV kernels) when available

@@ -146,10 +146,10 @@ class ModelRunner:
         self.part_tokens = cfg.decode_partition_tokens
         self.max_parts = max(1, math.ceil(cfg.max_model_len / self.part_tokens))
         # small decode batches split the context finer (more workgroups in flight for the
-        # latency-bound attention): partition tiers by batch size, finest first - tiny
-        # (<= decode_tiny_batch_max, 64 tokens: B = 1 at 0.6-3.5k context 7.3 / 8.8 us vs 8.4 /
-        # 10.7 at 128, profiles/r5_attention_partitions.txt) and small (<=
-        # decode_small_batch_max, 128 tokens); partial buffers are sized for the finest split
+        # latency-bound attention): partition tiers by batch size, finest first - the optional
+        # tiny tier (<= decode_tiny_batch_max, 64 tokens; off by default, see config.py) and
+        # small (<= decode_small_batch_max, 128 tokens); partial buffers are sized for the
+        # finest split
         self.part_tiers = []  # (max batch, partition tokens, max partitions, graph buckets)
         for mb, pt in ((cfg.decode_tiny_batch_max, cfg.decode_partition_tokens_tiny),
                        (cfg.decode_small_batch_max, cfg.decode_partition_tokens_small)):

@@ -20,9 +20,11 @@
 //   * per K step a wave applies its weight fragment (MFMA B operand) to all MT 16-row x
 //     fragments (A operand, ds_read_b128) - the weights are read once for every row;
 //   * the RMSNorm fold needs sum(x^2) per row: accumulated from the staged x registers;
-//   * split-K: each slice publishes its fp32 accumulators and partial sums of squares with
-//     device-scope (sc1) stores; the last arriving slice (arrival counter per column block)
-//     sums them in slice order - bitwise deterministic - and runs the epilogue.
+//   * split-K: each slice writes its fp32 row segments and partial sums of squares with
+//     plain stores and exits; a second launch (wide_reduce_kernel, one wave per tile) sums
+//     them in slice order - bitwise deterministic - and runs the epilogue.  (An in-launch
+//     last-arriver combine read every slice of a column block from ONE workgroup: 5-17 us
+//     at 85 rows against a 1.5 us launch boundary.)
 // One workgroup barrier per chunk.  Plain loads only (no LDS-DMA): mixing LDS-DMA with the
 // register weight stream makes hipcc wait vmcnt(0) at every weight use (cdna_hip_programming
 // §5, "Projection GEMM at M = 256" item 4(b)).
@@ -45,9 +47,9 @@ constexpr int kSlots = kRowB / 16;   // 16-B slots per staged row
 // split-K arrival counter, so they overlap the hand-over - and epi_apply computes and stores
 // 16-B row vectors.  (The GEMV's element-per-thread tile_epilogue, run by one wave over up to
 // 128 rows, paid one dependent load round trip per element: 24 per wave at 96 rows.)
-template <int MT>
+template <int RPL_>
 struct EpiIn {
-  static constexpr int RPL = MT * 16 > 64 ? 2 : 1;  // rows per lane
+  static constexpr int RPL = RPL_;  // rows per lane
   int rows[RPL];
   bool ok[RPL];
   u32x4 res[RPL][2];  // RESADD: the residual row segment (16 values)
@@ -57,14 +59,15 @@ struct EpiIn {
   uint64_t seed[RPL], step[RPL];
 };
 
-template <typename T, int EPI, int MT>
-__device__ __forceinline__ void epi_load(const SkinnyParams& p, const int tile, const int lane,
-                                         EpiIn<MT>& in) {
-  constexpr int RPL = EpiIn<MT>::RPL;
+// rows of this lane: row0 + lane + 64 j (j < RPL) for lanes < nl, rows < rmax and < p.M
+template <typename T, int EPI, int RPL>
+__device__ __forceinline__ void epi_load(const SkinnyParams& p, const int tile, const int row0,
+                                         const int nl, const int rmax, const int lane,
+                                         EpiIn<RPL>& in) {
 #pragma unroll
   for (int j = 0; j < RPL; ++j) {
-    in.rows[j] = lane + 64 * j;
-    in.ok[j] = in.rows[j] < MT * 16 && in.rows[j] < p.M;
+    in.rows[j] = row0 + lane + 64 * j;
+    in.ok[j] = lane < nl && in.rows[j] < rmax && in.rows[j] < p.M;
   }
   if constexpr (EPI == EPI_RESADD) {
 #pragma unroll
@@ -110,21 +113,22 @@ __device__ __forceinline__ u32x4 pack8(const uint16_t (&o)[8]) {
                o[4] | (uint32_t(o[5]) << 16), o[6] | (uint32_t(o[7]) << 16)};
 }
 
-template <typename T, int EPI, int MT>
+// red[m - rbase][n] holds row m's 16 accumulators, inv_rms[m - rbase] its norm scale
+template <typename T, int EPI, int RPL>
 __device__ __forceinline__ void epi_apply(const SkinnyParams& p, const int tile,
                                           const float (*red)[17], const float* inv_rms,
-                                          const bool norm, const EpiIn<MT>& in) {
-  constexpr int RPL = EpiIn<MT>::RPL;
+                                          const int rbase, const bool norm,
+                                          const EpiIn<RPL>& in) {
   if constexpr (EPI == EPI_PLAIN || EPI == EPI_RESADD) {
 #pragma unroll
     for (int j = 0; j < RPL; ++j) {
       if (!in.ok[j]) continue;
       const int m = in.rows[j];
-      const float sc = norm ? inv_rms[m] : 1.f;
+      const float sc = norm ? inv_rms[m - rbase] : 1.f;
       uint16_t o[2][8];
 #pragma unroll
       for (int n = 0; n < 16; ++n) {
-        float v = red[m][n] * sc;
+        float v = red[m - rbase][n] * sc;
         if constexpr (EPI == EPI_RESADD) {
           const uint32_t w = in.res[j][n >> 3][(n >> 1) & 3];
           v = to_f32<T>(from_f32<T>(v)) + to_f32<T>(static_cast<uint16_t>((n & 1) ? w >> 16 : w));
@@ -140,12 +144,12 @@ __device__ __forceinline__ void epi_apply(const SkinnyParams& p, const int tile,
     for (int j = 0; j < RPL; ++j) {
       if (!in.ok[j]) continue;
       const int m = in.rows[j];
-      const float sc = norm ? inv_rms[m] : 1.f;
+      const float sc = norm ? inv_rms[m - rbase] : 1.f;
       uint16_t o[8];
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
-        const float g = to_f32<T>(from_f32<T>(red[m][c] * sc));
-        const float u = to_f32<T>(from_f32<T>(red[m][c + 8] * sc));
+        const float g = to_f32<T>(from_f32<T>(red[m - rbase][c] * sc));
+        const float u = to_f32<T>(from_f32<T>(red[m - rbase][c + 8] * sc));
         const float si = to_f32<T>(from_f32<T>(g / (1.f + __expf(-g))));
         o[c] = from_f32<T>(si * u);
       }
@@ -159,13 +163,13 @@ __device__ __forceinline__ void epi_apply(const SkinnyParams& p, const int tile,
     for (int j = 0; j < RPL; ++j) {
       if (!in.ok[j]) continue;
       const int m = in.rows[j];
-      const float sc = norm ? inv_rms[m] : 1.f;
+      const float sc = norm ? inv_rms[m - rbase] : 1.f;
       uint16_t o1[8], o2[8];
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         // GEMM output rounded to T first (matches the unfused F.linear -> rope path)
-        const float x1 = to_f32<T>(from_f32<T>(red[m][c] * sc));
-        const float x2 = to_f32<T>(from_f32<T>(red[m][c + 8] * sc));
+        const float x1 = to_f32<T>(from_f32<T>(red[m - rbase][c] * sc));
+        const float x2 = to_f32<T>(from_f32<T>(red[m - rbase][c + 8] * sc));
         if (head < nq + nkv) {
           const float co = in.cs[j][c >> 2][c & 3], si = in.cs[j][2 + (c >> 2)][c & 3];
           o1[c] = from_f32<T>(x1 * co - x2 * si);
@@ -200,11 +204,11 @@ __device__ __forceinline__ void epi_apply(const SkinnyParams& p, const int tile,
     for (int j = 0; j < RPL; ++j) {
       if (!in.ok[j]) continue;
       const int m = in.rows[j];
-      const float sc = norm ? inv_rms[m] : 1.f;
+      const float sc = norm ? inv_rms[m - rbase] : 1.f;
       unsigned long long best = 0ull;
 #pragma unroll
       for (int n = 0; n < 16; ++n) {
-        float v = to_f32<T>(from_f32<T>(red[m][n] * sc));  // bf16 logits, as F.linear
+        float v = to_f32<T>(from_f32<T>(red[m - rbase][n] * sc));  // bf16 logits, as F.linear
         const int idx = p.vocab_offset + tile * 16 + n;    // global id: TP == TP1 noise
         if (in.temp[j] > 1e-5f)
           v = v / in.temp[j] + gumbel_noise(in.seed[j], in.step[j], static_cast<uint32_t>(idx));
@@ -233,7 +237,6 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDSB];
   __shared__ float ssq[R];
   __shared__ float inv_rms[R];
-  __shared__ int sk_last;
 
   // optional per-workgroup timeline (ops.set_gemv_trace, 100 MHz wall clock): [start, K loop
   // done, split-K partials published, end] at wg_trace[4 * (x + gridDim.x * y)]
@@ -388,84 +391,49 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
     }
   }
   __syncthreads();  // x buffers free from here on (the epilogue tiles reuse them)
-  // the epilogue's global inputs, in flight across the hand-over below
-  EpiIn<MT> ein;
-  epi_load<T, EPI, MT>(p, tvalid ? tile : 0, lane, ein);
-
-  if (S > 1) {
-    // ---- split-K hand-over: device-scope stores + arrival counter (common.h) -------------
-    const auto rws = dev_rsrc(p.sk_ws);
-    const uint32_t per_slice = static_cast<uint32_t>(WAVES * R * 16);
-    const uint32_t ss_base = static_cast<uint32_t>(gridDim.x * S) * per_slice;
-    const uint32_t mine = static_cast<uint32_t>(cb * S + ks) * per_slice +
-                          static_cast<uint32_t>(wid * R * 16 + col * R + 4 * grp);
-#pragma unroll
-    for (int t = 0; t < MT; ++t)
-      dev_store16(rws, (mine + 16 * t) * 4u, __builtin_bit_cast(u32x4, acc[t]));
-    if (norm && tid < R)
-      dev_store4(rws, (ss_base + static_cast<uint32_t>((cb * S + ks) * R + tid)) * 4u, ssq[tid]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores acknowledged
-    __syncthreads();
-    if (tid == 0) {
-      const int old = __hip_atomic_fetch_add(p.sk_counters + cb, 1, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-      sk_last = (old == S - 1);
-    }
-    __syncthreads();
-    if (p.wg_trace != nullptr) tr2 = wall_clock64();
-    if (!sk_last) {  // block-uniform
-      if (p.wg_trace != nullptr && tid == 0) {
-        unsigned long long* t = p.wg_trace + 4 * (blockIdx.x + gridDim.x * blockIdx.y);
-        t[0] = tr0;
-        t[1] = tr1;
-        t[2] = tr2;
-        t[3] = tr2;
-      }
-      return;
-    }
-    const uint32_t first = static_cast<uint32_t>(cb * S) * per_slice +
-                           static_cast<uint32_t>(wid * R * 16 + col * R + 4 * grp);
-    // QB slices' partials in flight per round trip (<= 32 16-B loads per lane: S <= 4 at 128
-    // rows, S <= 8 below 80 - one round trip), summed in slice order: deterministic
-    constexpr int QB = MT <= 4 ? 8 : MT <= 6 ? 5 : 4;
-#pragma unroll
-    for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int q0 = 0; q0 < S; q0 += QB) {
-      f32x4 part[QB][MT];
-#pragma unroll
-      for (int u = 0; u < QB; ++u) {
-        const int q = min(q0 + u, S - 1);
-#pragma unroll
-        for (int t = 0; t < MT; ++t)
-          part[u][t] = __builtin_bit_cast(
-              f32x4, dev_load16(rws, (first + q * per_slice + 16 * t) * 4u));
-      }
-#pragma unroll
-      for (int u = 0; u < QB; ++u)
-#pragma unroll
-        for (int t = 0; t < MT; ++t) acc[t] += (q0 + u < S) ? part[u][t] : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    if (norm && tid < R) {
-      float part[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        part[u] = dev_load4(rws, (ss_base + static_cast<uint32_t>((cb * S + min(u, S - 1)) * R + tid)) * 4u);
-      float sum = 0.f;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) sum += u < S ? part[u] : 0.f;  // S <= 8 (plan)
-      ssq[tid] = sum;
-    }
-    if (tid == 0)
-      __hip_atomic_store(p.sk_counters + cb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (norm && tid < R) inv_rms[tid] = rsqrtf(ssq[tid] / static_cast<float>(p.K) + p.eps);
   float(*red)[17] = reinterpret_cast<float(*)[17]>(lds + wid * R * 17 * 4);
 #pragma unroll
   for (int t = 0; t < MT; ++t)
 #pragma unroll
     for (int i = 0; i < 4; ++i) red[t * 16 + 4 * grp + i][col] = acc[t][i];
+  if (S > 1) {
+    // ---- split-K: publish this slice's rows (plain stores: the reduce launch that follows
+    // in stream order combines them - no in-launch hand-over, no last-arriver serial read of
+    // every slice's slab: 5-17 us at 85 rows, profiles/r5_wide_gemm.txt) ------------------
+    __syncthreads();
+    if (tvalid) {
+#pragma unroll
+      for (int j = 0; j < (R > 64 ? 2 : 1); ++j) {
+        const int row = lane + 64 * j;
+        if (row < R && row < p.M) {
+          float* dst = p.sk_ws + ((static_cast<int64_t>(tile) * S + ks) * R + row) * 16;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            reinterpret_cast<f32x4*>(dst)[q] =
+                f32x4{red[row][4 * q], red[row][4 * q + 1], red[row][4 * q + 2], red[row][4 * q + 3]};
+        }
+      }
+    }
+    if (norm && tid < R && tid < p.M)
+      p.sk_ws[static_cast<int64_t>(ntiles) * S * R * 16 + (static_cast<int64_t>(cb) * S + ks) * R + tid] =
+          ssq[tid];
+    if (p.wg_trace != nullptr) {
+      if (tid == 0) {
+        unsigned long long* t = p.wg_trace + 4 * (blockIdx.x + gridDim.x * blockIdx.y);
+        t[0] = tr0;
+        t[1] = tr1;
+        t[2] = wall_clock64();
+        t[3] = t[2];
+      }
+    }
+    return;
+  }
+  // the epilogue's global inputs
+  EpiIn<(R > 64 ? 2 : 1)> ein;
+  epi_load<T, EPI, (R > 64 ? 2 : 1)>(p, tvalid ? tile : 0, 0, 64, R, lane, ein);
+  if (norm && tid < R) inv_rms[tid] = rsqrtf(ssq[tid] / static_cast<float>(p.K) + p.eps);
   __syncthreads();
-  if (tvalid) epi_apply<T, EPI, MT>(p, tile, red, inv_rms, norm, ein);
+  if (tvalid) epi_apply<T, EPI, (R > 64 ? 2 : 1)>(p, tile, red, inv_rms, 0, norm, ein);
   if (p.wg_trace != nullptr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -476,6 +444,87 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
       t[2] = tr2;
       t[3] = wall_clock64();
     }
+  }
+}
+
+// Split-K combine + epilogue: one wave per (16-column tile, 16-row group); lane l loads
+// columns 4 (l >> 4) .. +3 of row (l & 15) from every slice (16 B each, all issued together:
+// one round trip for S <= 8), sums them in slice order - bitwise deterministic - with the row
+// sums of squares, and lanes 0-15 run the unsplit path's epi_apply on their row.  (One wave
+// per tile over all rows left most CUs idle: 10 us.)
+template <typename T, int MT, int EPI, bool NORM>
+__global__ __launch_bounds__(256) void wide_reduce_kernel(SkinnyParams p, int ntiles, int S,
+                                                         int waves) {
+  constexpr int R = MT * 16;
+  __shared__ float red_all[4][16][17];
+  __shared__ float inv_all[4][16];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int gw = blockIdx.x * 4 + wid;
+  const int tile = gw / MT, rg = gw % MT;
+  if (tile >= ntiles) return;  // wave-uniform; no workgroup barrier below
+  const int cb = tile / waves;
+  const int r = rg * 16 + (lane & 15), qd = lane >> 4;
+  const int rc = min(r, max(p.M - 1, 0));
+  EpiIn<1> ein;
+  epi_load<T, EPI, 1>(p, tile, rg * 16, 16, R, lane, ein);
+  f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+  float ss = 0.f;
+  for (int k0 = 0; k0 < S; k0 += 8) {
+    f32x4 part[8];
+    float sp[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int ks = min(k0 + u, S - 1);
+      part[u] = reinterpret_cast<const f32x4*>(
+          p.sk_ws + ((static_cast<int64_t>(tile) * S + ks) * R + rc) * 16)[qd];
+      if constexpr (NORM)
+        sp[u] = p.sk_ws[static_cast<int64_t>(ntiles) * S * R * 16 +
+                        (static_cast<int64_t>(cb) * S + ks) * R + rc];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool real = k0 + u < S;
+      sum += real ? part[u] : f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (NORM) ss += real ? sp[u] : 0.f;
+    }
+  }
+  float(*red)[17] = red_all[wid];
+  float* inv_rms = inv_all[wid];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) red[lane & 15][4 * qd + e] = sum[e];
+  if (NORM && qd == 0) inv_rms[lane & 15] = rsqrtf(ss / static_cast<float>(p.K) + p.eps);
+  __builtin_amdgcn_wave_barrier();  // rows were written by 4 lanes each: in-wave hand-over
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  epi_apply<T, EPI, 1>(p, tile, red, inv_rms, rg * 16, NORM, ein);
+}
+
+template <typename T, int MT>
+static int launch_reduce(int epi, const SkinnyParams& p, int ntiles, int S, int waves,
+                         hipStream_t st) {
+  const dim3 grid((ntiles * MT + 3) / 4), blk(256);
+  const bool norm = p.eps > 0.f;
+  switch (epi) {
+    case EPI_PLAIN: wide_reduce_kernel<T, MT, EPI_PLAIN, false><<<grid, blk, 0, st>>>(p, ntiles, S, waves); return 0;
+    case EPI_RESADD: wide_reduce_kernel<T, MT, EPI_RESADD, false><<<grid, blk, 0, st>>>(p, ntiles, S, waves); return 0;
+    case EPI_QKVROPE: wide_reduce_kernel<T, MT, EPI_QKVROPE, true><<<grid, blk, 0, st>>>(p, ntiles, S, waves); return 0;
+    case EPI_SILU: wide_reduce_kernel<T, MT, EPI_SILU, true><<<grid, blk, 0, st>>>(p, ntiles, S, waves); return 0;
+    case EPI_SAMPLE:
+      if (norm) wide_reduce_kernel<T, MT, EPI_SAMPLE, true><<<grid, blk, 0, st>>>(p, ntiles, S, waves);
+      else wide_reduce_kernel<T, MT, EPI_SAMPLE, false><<<grid, blk, 0, st>>>(p, ntiles, S, waves);
+      return 0;
+    default: return -1;
+  }
+}
+
+template <typename T>
+static int launch_reduce_mt(int epi, int mt, const SkinnyParams& p, int ntiles, int S,
+                            int waves, hipStream_t st) {
+  switch (mt) {
+    case 2: return launch_reduce<T, 2>(epi, p, ntiles, S, waves, st);
+    case 4: return launch_reduce<T, 4>(epi, p, ntiles, S, waves, st);
+    case 6: return launch_reduce<T, 6>(epi, p, ntiles, S, waves, st);
+    case 8: return launch_reduce<T, 8>(epi, p, ntiles, S, waves, st);
+    default: return -1;
   }
 }
 
@@ -545,9 +594,8 @@ static int launch_mt(int epi, int mt, int waves, dim3 grid, hipStream_t st,
 
 // Grid plan: per candidate wave count (tiles per workgroup) and K split S <= 8, a time
 // estimate - rounds of the grid over the CUs x (a workgroup's weight bytes + x bytes / 3 at a
-// per-CU streaming rate, plus ~1.5 us of ramp), plus the split-K hand-over (~1 us + 0.4 us
-// per slice the last arriver reads back) - and the cheapest wins.  Slices keep >= 2 chunks
-// of K.
+// per-CU streaming rate, plus ~1.5 us of ramp), plus for a split the reduce launch - and the
+// cheapest wins.  Slices keep >= 2 chunks of K.
 static void plan(int ntiles, int K, int M, bool norm, int& waves, int& ksplit) {
   constexpr double kCUs = 256.0, kBpus = 24e3;  // bytes per us per CU
   const int mpad = ((M + 15) / 16) * 16;
@@ -563,8 +611,10 @@ static void plan(int ntiles, int K, int M, bool norm, int& waves, int& ksplit) {
       const double kslice = static_cast<double>(K) / s;
       const double bytes = w * 16.0 * kslice * 2.0 + mpad * kslice * 2.0 / 3.0;
       const double idle = static_cast<double>(ncb * w - ntiles) / (ncb * w);  // empty waves
+      // split: a reduce launch (~2 us incl. its boundary) reading every slice's slab
+      const double slab = static_cast<double>(ntiles) * s * mpad * 64.0;
       const double t = rounds * (bytes / kBpus * (1.0 + 0.5 * idle) + 1.5) +
-                       (s > 1 ? 1.0 + 0.4 * s : 0.0);
+                       (s > 1 ? 2.0 + slab / 5e6 : 0.0);
       if (t < best - 1e-9) {
         best = t;
         waves = w;
@@ -592,21 +642,29 @@ int atta_wide_launch(SkinnyParams& p, int epi, int ntiles, int waves, int ksplit
   if (ksplit < 1 || p.K / wide::kKC < ksplit) return -1;
   const int mt = p.M <= 32 ? 2 : p.M <= 64 ? 4 : p.M <= 96 ? 6 : 8;
   const int ncb = (ntiles + waves - 1) / waves;
-  // a split whose slabs do not fit the workspace is halved until they do
+  // slices' row segments [tile][slice][row][16] + row sums of squares [cb][slice][row]; a
+  // split whose slabs do not fit the workspace is halved until they do
   auto need = [&](int s) {
-    return static_cast<int64_t>(ncb) * s * waves * mt * 16 * 16 +
+    return static_cast<int64_t>(ntiles) * s * mt * 16 * 16 +
            static_cast<int64_t>(ncb) * s * mt * 16;
   };
   while (ksplit > 1 && need(ksplit) > ws_floats) ksplit >>= 1;
   if (ksplit > 1) {
-    if (sk_ws == nullptr || ncb > n_counters) return -2;
+    if (sk_ws == nullptr) return -2;
     p.sk_ws = const_cast<float*>(sk_ws);
     p.sk_counters = sk_counters;
   }
+  (void)n_counters;
   p.ksplit = ksplit;
   const dim3 grid(ncb, ksplit);
-  const int rc = dtype == 0 ? wide::launch_mt<__bf16>(epi, mt, waves, grid, stream, p, ntiles)
-                            : wide::launch_mt<_Float16>(epi, mt, waves, grid, stream, p, ntiles);
+  int rc = dtype == 0 ? wide::launch_mt<__bf16>(epi, mt, waves, grid, stream, p, ntiles)
+                      : wide::launch_mt<_Float16>(epi, mt, waves, grid, stream, p, ntiles);
   if (rc) return rc;
+  if (ksplit > 1) {
+    p.wg_trace = nullptr;
+    rc = dtype == 0 ? wide::launch_reduce_mt<__bf16>(epi, mt, p, ntiles, ksplit, waves, stream)
+                    : wide::launch_reduce_mt<_Float16>(epi, mt, p, ntiles, ksplit, waves, stream);
+    if (rc) return rc;
+  }
   return static_cast<int>(hipGetLastError());
 }

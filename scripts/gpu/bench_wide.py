@@ -4,7 +4,7 @@ Cache), with the fused epilogues the engine uses (qkv: norm + RoPE + K/V write, 
 residual add, gate_up: norm + SiLU-mul).  Library column = F.linear (hipBLASLt) on row-major
 weights plus the separate norm / RoPE / SiLU kernels it needs.
 
-    python scripts/gpu/bench_wide.py [--m 33 85 128] [--plans]
+    python scripts/gpu/bench_wide.py [--m 33 85 128] [--plans] [--graph]
 """
 import argparse
 import os
@@ -24,16 +24,36 @@ PLANS = {"qkv": [(6, 4), (8, 4), (6, 2), (4, 4), (8, 6)],
          "down": [(8, 8), (4, 4), (8, 4), (4, 8), (8, 16)]}
 
 
+GRAPH = False
+
+
 def timeit(fn, n=30, reps=3):
+    """us per call over n back-to-back calls; with --graph the n calls are captured in one
+    hipGraph and replayed (GPU time incl. launch gaps, no host launch cost - the decode
+    step's regime), else launched eagerly (the prefill step's regime)."""
     for i in range(3):
         fn(i)
     torch.cuda.synchronize()
+    g = None
+    if GRAPH:
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+            for i in range(n):
+                fn(i)
+        torch.cuda.current_stream().wait_stream(s)
+        g.replay()
+        torch.cuda.synchronize()
     out = []
     for _ in range(reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        for i in range(n):
-            fn(i)
+        if g is not None:
+            g.replay()
+        else:
+            for i in range(n):
+                fn(i)
         e1.record()
         torch.cuda.synchronize()
         out.append(e0.elapsed_time(e1) * 1e3 / n)
@@ -45,7 +65,10 @@ def main():
     ap.add_argument("--m", type=int, nargs="+", default=[33, 48, 64, 85, 96, 128])
     ap.add_argument("--plans", action="store_true", help="also sweep (waves, split) plans")
     ap.add_argument("--proj", nargs="+", default=list(SHAPES))
+    ap.add_argument("--graph", action="store_true", help="time graph replays (no host cost)")
     a = ap.parse_args()
+    global GRAPH
+    GRAPH = a.graph
     assert ops.native_available(), ops._load_error
     ops.ensure_splitk_workspace("cuda")
     dt = torch.bfloat16
@@ -99,9 +122,13 @@ def main():
             line = (f"{proj:8s} M={m:4d} | wide {tw:7.1f} us ({mb / tw:5.2f} TB/s) | "
                     f"library {tl:7.1f} us | {tl / tw:5.2f}x")
             if a.plans:
-                line += " | plans " + " ".join(
-                    f"{w_}x{s_}={timeit(lambda i, p=(w_, s_): wide(i, p)):.1f}"
-                    for w_, s_ in PLANS[proj])
+                cells = []
+                for w_, s_ in PLANS[proj]:
+                    try:
+                        cells.append(f"{w_}x{s_}={timeit(lambda i, p=(w_, s_): wide(i, p)):.1f}")
+                    except RuntimeError:  # a plan the library does not build at this M
+                        cells.append(f"{w_}x{s_}=n/a")
+                line += " | plans " + " ".join(cells)
             print(line, flush=True)
         del raw, wps
         torch.cuda.empty_cache()

@@ -106,6 +106,7 @@ def test_parts_buckets_cover_context():
     cfg = EngineConfig(model="tiny", device="cpu", max_model_len=3000, num_kv_blocks=64)
     r = LLMEngine(cfg).runner
     assert r.max_parts == 12 and r.parts_buckets == [1, 2, 4, 6, 8, 12]
+    assert [r._tier(b)[0] for b in (1, 2, 8, 9)] == [128, 128, 128, 256]  # tiny tier off
     prev = 0
     for kv in range(1, 3001):
         p = r.parts_bucket(kv)
@@ -122,9 +123,9 @@ def test_parts_buckets_cover_context():
     assert r.parts_bucket(1025, 4) == 6
     for kv in range(1, 3001, 7):
         assert r.parts_bucket(kv, 1) * 128 >= kv and r.parts_bucket(kv, 3) * 256 >= kv
-    # three tiers (the defaults): 64-token partitions for B <= 2, 128 for B <= 8, 256 above
+    # three tiers (tiny enabled): 64-token partitions for B <= 2, 128 for B <= 8, 256 above
     r = LLMEngine(EngineConfig(model="tiny", device="cpu", max_model_len=3000,
-                               num_kv_blocks=64)).runner
+                               num_kv_blocks=64, decode_tiny_batch_max=2)).runner
     assert [r._tier(b)[0] for b in (1, 2, 3, 8, 9)] == [64, 64, 128, 128, 256]
     assert r._tier(1)[1] == 47 and r.parts_bucket(1025, 1) == 24  # ceil(1025 / 64) = 17
     for kv in range(1, 3001, 7):
@@ -234,12 +235,11 @@ def test_special_sampling_graphs_equal_eager():
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["bucket64", "unfused_special"])
 def test_unfused_graph_buckets_equal_eager(case):
-    """graph replays of the non-fused decode path must leave the sampled
-    tokens in ws["tokens"] (where launch() reads them and the look-ahead step embeds them).
-    bucket64: 40 sequences replay the 64-bucket graph, past the fused GEMV limit (32 rows),
-    so the step is forward() + LM head + sampler; unfused_special: max_model_len 20000 turns
-    the fused decode path off and every row uses top-p / top-k.  Graph == eager, token for
-    token."""
+    """graph replays must leave the sampled tokens in ws["tokens"] (where
+    launch() reads them and the look-ahead step embeds them).  bucket64: 40 sequences replay
+    the 64-bucket graph (the wide small-M kernels since round 5); unfused_special:
+    max_model_len 20000 turns the fused decode path off and every row uses top-p / top-k, so
+    the step is forward() + LM head + sampler.  Graph == eager, token for token."""
     rng = np.random.default_rng(21)
     if case == "bucket64":
         prompts = [rng.integers(300, 30000, size=int(n)).tolist()
@@ -267,6 +267,27 @@ def test_unfused_graph_buckets_equal_eager(case):
         del eng
         torch.cuda.empty_cache()
     assert res[0] == res[1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nseq", [48, 64, 100])
+def test_wide_fused_decode_matches_oracle(nseq):
+    """decode batches of 33-128 sequences run the fused path (wide small-M
+    GEMM with the norm-fold / RoPE + KV write / SiLU / residual / sampler epilogues) inside the
+    batch bucket's hipGraph, and every generated position matches the fp32 dense oracle
+    teacher-forced."""
+    rng = np.random.default_rng(nseq)
+    prompts = [rng.integers(300, 30000, size=int(n)).tolist()
+               for n in rng.integers(3, 40, size=nseq)]
+    eng = LLMEngine(EngineConfig(model="small", device="cuda", max_model_len=512,
+                                 num_kv_blocks=2048, max_num_seqs=nseq,
+                                 max_num_batched_tokens=4096,
+                                 graph_batch_sizes=(1, 2, 4, 8, 16, 32, 64, 128)))
+    assert eng.runner.fused_decode and eng.runner.model.decode_fusable(nseq)
+    _check(eng, prompts, n=4, tol_logit=0.25)
+    bucket = 64 if nseq <= 64 else 128
+    assert any(k[0] == bucket for k in eng.runner.graphs), sorted(eng.runner.graphs)
+    assert eng.runner.graph_steps > 0
 
 
 @pytest.mark.gpu
