@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--plans", action="store_true", help="also sweep (waves, split) plans")
     ap.add_argument("--proj", nargs="+", default=list(SHAPES))
     ap.add_argument("--graph", action="store_true", help="time graph replays (no host cost)")
+    ap.add_argument("--sweep", action="store_true",
+                    help="every (waves, split) plan; prints the best per (proj, M)")
     a = ap.parse_args()
     global GRAPH
     GRAPH = a.graph
@@ -121,6 +123,18 @@ def main():
             tot[m][1] += tl
             line = (f"{proj:8s} M={m:4d} | wide {tw:7.1f} us ({mb / tw:5.2f} TB/s) | "
                     f"library {tl:7.1f} us | {tl / tw:5.2f}x")
+            if a.sweep:
+                tim = {}
+                for w_ in (4, 6, 7, 8):
+                    for s_ in (1, 2, 3, 4, 5, 6, 8):
+                        try:
+                            tim[(w_, s_)] = timeit(lambda i, p=(w_, s_): wide(i, p), n=20)
+                        except RuntimeError as e:
+                            err = str(e).splitlines()[0]
+                assert tim, f"no plan ran: {err}"
+                best = min(tim, key=tim.get)
+                line += (f" | best {best[0]}x{best[1]}={tim[best]:.1f} | " +
+                         " ".join(f"{k[0]}x{k[1]}={v:.1f}" for k, v in sorted(tim.items())))
             if a.plans:
                 cells = []
                 for w_, s_ in PLANS[proj]:
