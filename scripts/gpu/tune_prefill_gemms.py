@@ -6,6 +6,7 @@ prefill streams them).  Writes agentic_traffic_testing_amd/tuning/tunableop_gfx9
 (or --out); the engine loads it lookup-only (EngineConfig.gemm_tuning).
 
     python scripts/gpu/tune_prefill_gemms.py --model llama-3.1-8b --max-rows 8192
+    python scripts/gpu/tune_prefill_gemms.py --model llama-3-70b --tp 8 --buckets 16,96,384
 """
 import argparse
 import os
@@ -27,14 +28,21 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--duration-ms", type=int, default=40,
                     help="TunableOp time per candidate solution")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tune the per-rank shard shapes of this TP degree (column-parallel "
+                         "qkv / gate_up: N / tp; row-parallel o / down: K / tp)")
+    ap.add_argument("--buckets", default="",
+                    help="comma-separated row buckets instead of every bucket in range")
     a = ap.parse_args()
     mc = resolve_model(a.model)[0]
     out = a.out or str(tuning.table_path(mc.name))
+    tp = a.tp
     H, I = mc.hidden_size, mc.intermediate_size
     qkv_n = (mc.num_heads + 2 * mc.num_kv_heads) * mc.head_dim
     o_k = mc.num_heads * mc.head_dim
-    shapes = {"qkv": (qkv_n, H, False), "o": (H, o_k, True), "gate_up": (2 * I, H, False),
-              "down": (H, I, True)}
+    assert qkv_n % tp == 0 and o_k % tp == 0 and I % tp == 0, "shapes not divisible by --tp"
+    shapes = {"qkv": (qkv_n // tp, H, False), "o": (H, o_k // tp, True),
+              "gate_up": (2 * I // tp, H, False), "down": (H, I // tp, True)}
     tun = torch.cuda.tunable
     tun.enable(True)
     tun.tuning_enable(True)
@@ -42,8 +50,10 @@ def main():
     tun.set_filename(out)
     tun.set_max_tuning_duration(a.duration_ms)
     tun.set_rotating_buffer_size(512)  # MB: candidates run on rotating operand copies
-    buckets = [b for b in tuning.all_buckets(a.max_rows) if b >= a.min_rows]
-    print(f"# tuning {a.model}: {len(shapes)} projections x {len(buckets)} row buckets "
+    buckets = ([int(b) for b in a.buckets.split(",")] if a.buckets else
+               [b for b in tuning.all_buckets(a.max_rows) if b >= a.min_rows])
+    assert all(tuning.bucket_rows(b) == b for b in buckets), "not a row bucket"
+    print(f"# tuning {a.model} TP={tp}: {len(shapes)} projections x {len(buckets)} row buckets "
           f"({buckets[0]}..{buckets[-1]}) -> {out}", flush=True)
     t0 = time.time()
     ws = {k: (torch.rand(n, kk, device="cuda") * 2 - 1).to(torch.bfloat16) / kk ** 0.5
