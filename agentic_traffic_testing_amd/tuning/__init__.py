@@ -37,8 +37,13 @@ def all_buckets(max_rows: int) -> list[int]:
     return out
 
 
+# presets with the same GEMM shapes share a table (TunableOp keys entries by exact shape; one
+# file holds a model's TP=1 shapes and its TP=8 shard shapes)
+TABLE_ALIASES = {"llama-3-8b": "llama-3.1-8b", "llama-3.1-70b": "llama-3-70b"}
+
+
 def table_path(model_name: str, arch: str = "gfx950") -> Path:
-    return HERE / f"tunableop_{arch}_{model_name}.csv"
+    return HERE / f"tunableop_{arch}_{TABLE_ALIASES.get(model_name, model_name)}.csv"
 
 
 _loaded: str | None = None

@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--tp", type=int, default=1,
                     help="tune the per-rank shard shapes of this TP degree (column-parallel "
                          "qkv / gate_up: N / tp; row-parallel o / down: K / tp)")
+    ap.add_argument("--fp8", action="store_true",
+                    help="tune the fp8 prefill GEMMs (row-wise scaled torch._scaled_mm, as "
+                         "ops.gemm_fp8 calls it) instead of the bf16 ones")
     ap.add_argument("--buckets", default="",
                     help="comma-separated row buckets instead of every bucket in range")
     a = ap.parse_args()
@@ -58,10 +61,17 @@ def main():
     t0 = time.time()
     ws = {k: (torch.rand(n, kk, device="cuda") * 2 - 1).to(torch.bfloat16) / kk ** 0.5
           for k, (n, kk, _) in shapes.items()}
+    f8 = torch.float8_e4m3fn
+    w8 = {k: (w.float() * 8).to(f8) for k, w in ws.items()} if a.fp8 else {}
     for m in buckets:
         for name, (n, k, res) in shapes.items():
             x = (torch.rand(m, k, device="cuda") * 2 - 1).to(torch.bfloat16)
-            if res:
+            if a.fp8:
+                torch._scaled_mm(x.to(f8), w8[name].t(),
+                                 scale_a=torch.rand(m, 1, device="cuda") + 0.5,
+                                 scale_b=torch.rand(1, n, device="cuda") + 0.5,
+                                 out_dtype=torch.bfloat16)
+            elif res:
                 r = torch.zeros(m, n, device="cuda", dtype=torch.bfloat16)
                 r.addmm_(x, ws[name].t())
             else:
