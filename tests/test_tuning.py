@@ -61,3 +61,36 @@ def test_prefill_impl_falls_back_past_flash_table_width():
             ops.prefill_tile_tokens(4, "v1")
     with pytest.raises(ValueError):
         ops.prefill_impl(ops.FLASH_MAX_BT + 1, "flash")
+
+
+def _table_shapes(path):
+    """{(op kind, m, n, k)} of a TunableOp CSV (tn_<n>_<m>_<k>_...)."""
+    out = set()
+    for line in open(path):
+        p = line.rstrip("\n").split(",")
+        if p[0] == "Validator" or len(p) < 4:
+            continue
+        n, m, k = (int(v) for v in p[1].split("_")[1:4])
+        out.add(("fp8" if p[0].startswith("Scaled") else "bf16", m, n, k))
+    return out
+
+
+def test_shipped_tables_cover_every_bucket_and_shard():
+    """the shipped tables hold every projection's GEMM at every row bucket up
+    to 4096 - the 8B (bf16 and fp8) and the 70B at TP=1 and its TP=8 per-rank shard shapes
+    (column-parallel qkv / gate_up split N, row-parallel o / down split K), bf16 and fp8."""
+    from agentic_traffic_testing_amd.config import resolve_model
+    buckets = tuning.all_buckets(4096)
+    for model, tps in (("llama-3.1-8b", (1,)), ("llama-3-70b", (1, 8)),
+                       ("llama-3.1-70b", (1, 8))):
+        mc = resolve_model(model)[0]
+        have = _table_shapes(tuning.table_path(mc.name))
+        H, I = mc.hidden_size, mc.intermediate_size
+        qkv = (mc.num_heads + 2 * mc.num_kv_heads) * mc.head_dim
+        o_k = mc.num_heads * mc.head_dim
+        for tp in tps:
+            shapes = [(qkv // tp, H), (H, o_k // tp), (2 * I // tp, H), (H, I // tp)]
+            for kind in ("bf16", "fp8"):
+                miss = [(m, n, k) for m in buckets for n, k in shapes
+                        if (kind, m, n, k) not in have]
+                assert not miss, (model, tp, kind, miss[:4])
