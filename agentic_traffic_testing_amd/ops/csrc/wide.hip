@@ -521,11 +521,18 @@ static int launch_reduce_mt(int epi, int mt, const SkinnyParams& p, int ntiles, 
                             int waves, hipStream_t st) {
   switch (mt) {
     case 2: return launch_reduce<T, 2>(epi, p, ntiles, S, waves, st);
+    case 3: return launch_reduce<T, 3>(epi, p, ntiles, S, waves, st);
     case 4: return launch_reduce<T, 4>(epi, p, ntiles, S, waves, st);
+    case 5: return launch_reduce<T, 5>(epi, p, ntiles, S, waves, st);
     case 6: return launch_reduce<T, 6>(epi, p, ntiles, S, waves, st);
+    case 7: return launch_reduce<T, 7>(epi, p, ntiles, S, waves, st);
     case 8: return launch_reduce<T, 8>(epi, p, ntiles, S, waves, st);
     default: return -1;
   }
+}
+
+constexpr bool norm_fits(int waves, int mt) {
+  return !((mt == 8 && (waves == 6 || waves == 7)) || (mt == 7 && waves == 6));
 }
 
 // RMSNorm fold per epilogue as the engine uses them: never for the plain / residual
@@ -535,8 +542,9 @@ template <typename T, int WAVES, int MT>
 static int launch_epi(int epi, dim3 grid, hipStream_t st, const SkinnyParams& p, int ntiles) {
   const dim3 blk(WAVES * 64);
   const bool norm = p.eps > 0.f;
-  // 6 / 7 waves at 128 rows with the norm fold spill past 256 VGPRs (the plan avoids them)
-  constexpr bool kNormOk = !(MT == 8 && (WAVES == 6 || WAVES == 7));
+  // 6 / 7 waves at 128 rows and 6 waves at 112 rows with the norm fold spill past 256 VGPRs
+  // (the plan avoids them)
+  constexpr bool kNormOk = norm_fits(WAVES, MT);
   if constexpr (!kNormOk) {
     if (norm) return -1;
   }
@@ -585,8 +593,11 @@ static int launch_mt(int epi, int mt, int waves, dim3 grid, hipStream_t st,
                      const SkinnyParams& p, int ntiles) {
   switch (mt) {
     case 2: return launch_w<T, 2>(epi, waves, grid, st, p, ntiles);
+    case 3: return launch_w<T, 3>(epi, waves, grid, st, p, ntiles);
     case 4: return launch_w<T, 4>(epi, waves, grid, st, p, ntiles);
+    case 5: return launch_w<T, 5>(epi, waves, grid, st, p, ntiles);
     case 6: return launch_w<T, 6>(epi, waves, grid, st, p, ntiles);
+    case 7: return launch_w<T, 7>(epi, waves, grid, st, p, ntiles);
     case 8: return launch_w<T, 8>(epi, waves, grid, st, p, ntiles);
     default: return -1;
   }
@@ -604,7 +615,7 @@ static void plan(int ntiles, int K, int M, bool norm, int& waves, int& ksplit) {
   const int ws[4] = {4, 6, 7, 8};
   for (int wi = 0; wi < 4; ++wi) {
     const int w = ws[wi];
-    if (norm && M > 96 && (w == 6 || w == 7)) continue;  // see launch_epi
+    if (norm && !norm_fits(w, M <= 32 ? 2 : (M + 15) / 16)) continue;  // see launch_epi
     const int ncb = (ntiles + w - 1) / w;
     for (int s = 1; s <= 8 && nch / s >= 2; ++s) {
       const double rounds = std::ceil(ncb * s / kCUs);
@@ -640,7 +651,8 @@ int atta_wide_launch(SkinnyParams& p, int epi, int ntiles, int waves, int ksplit
   if (waves <= 0 || ksplit <= 0) wide::plan(ntiles, p.K, p.M, p.eps > 0.f, waves, ksplit);
   if (waves != 4 && waves != 6 && waves != 7 && waves != 8) return -1;
   if (ksplit < 1 || p.K / wide::kKC < ksplit) return -1;
-  const int mt = p.M <= 32 ? 2 : p.M <= 64 ? 4 : p.M <= 96 ? 6 : 8;
+  // 16-row blocks: rows padded to the next 16 only (75 rows: 80, not 96)
+  const int mt = p.M <= 32 ? 2 : (p.M + 15) / 16;
   const int ncb = (ntiles + waves - 1) / waves;
   // slices' row segments [tile][slice][row][16] + row sums of squares [cb][slice][row]; a
   // split whose slabs do not fit the workspace is halved until they do

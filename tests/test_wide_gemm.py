@@ -29,13 +29,21 @@ def close(a, b, atol, rtol=0.0):
     assert bool((err <= tol).all()), f"max err {err.max().item():.4g}"
 
 
+def _norm_fits(waves, m):
+    """Plans built with the RMSNorm fold (wide.hip norm_fits): 6 / 7 waves spill at 113-128
+    rows, 6 waves at 97-112."""
+    mt = (m + 15) // 16
+    return not ((mt == 8 and waves in (6, 7)) or (mt == 7 and waves == 6))
+
+
 def _norm_ref(x, eps=1e-5):
     return ref.rms_norm(x, torch.ones(x.shape[1], dtype=x.dtype, device=x.device), eps)
 
 
 @pytest.mark.parametrize("plan", PLANS)
 @pytest.mark.parametrize("m,n,k", [(33, 1024, 4096), (85, 4096, 4096), (128, 512, 14336),
-                                   (47, 6144, 1024), (96, 2048, 2048)])
+                                   (47, 6144, 1024), (96, 2048, 2048), (75, 4096, 4096),
+                                   (110, 2048, 2048)])
 def test_wide_linear_plain_and_residual(plan, m, n, k):
     torch.manual_seed(41)
     dt = torch.bfloat16
@@ -64,11 +72,11 @@ def test_wide_linear_plain_and_residual(plan, m, n, k):
 
 
 @pytest.mark.parametrize("plan", [(0, 0), (6, 4), (8, 1), (4, 3)])
-@pytest.mark.parametrize("m", [33, 85, 128])
+@pytest.mark.parametrize("m", [33, 75, 85, 100, 128])
 @pytest.mark.parametrize("hq,hkv,H", [(32, 8, 4096), (8, 1, 8192)])
 def test_wide_qkv_rope(plan, m, hq, hkv, H):
-    if m > 96 and plan[0] in (6, 7):
-        pytest.skip("6 / 7 waves x 128 rows with the norm fold is not built (VGPR spill)")
+    if not _norm_fits(plan[0], m):
+        pytest.skip("this wave count x row count with the norm fold is not built (VGPR spill)")
     torch.manual_seed(42)
     dt, bs, nb = torch.bfloat16, 16, 64
     x = torch.randn(m, H, dtype=dt, device="cuda") * 2
@@ -91,11 +99,11 @@ def test_wide_qkv_rope(plan, m, hq, hkv, H):
 
 
 @pytest.mark.parametrize("plan", [(0, 0), (7, 1), (8, 2), (4, 4)])
-@pytest.mark.parametrize("m", [40, 85, 128])
+@pytest.mark.parametrize("m", [40, 75, 85, 100, 128])
 @pytest.mark.parametrize("inter,k", [(14336, 4096), (1792, 8192)])
 def test_wide_gate_up_silu(plan, m, inter, k):
-    if m > 96 and plan[0] in (6, 7):
-        pytest.skip("6 / 7 waves x 128 rows with the norm fold is not built (VGPR spill)")
+    if not _norm_fits(plan[0], m):
+        pytest.skip("this wave count x row count with the norm fold is not built (VGPR spill)")
     torch.manual_seed(43)
     dt = torch.bfloat16
     x = torch.randn(m, k, dtype=dt, device="cuda")
