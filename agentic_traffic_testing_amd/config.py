@@ -233,7 +233,8 @@ class EngineConfig:
     # prefill projection GEMMs: "hipblaslt", "atta" (hand-written CDNA4 Stream-K GEMM with
     # fused residual-add / SiLU-mul epilogues, bf16 and fp8: ops/csrc/prefill_gemm.hip, for
     # steps of >= prefill_gemm_min_rows tokens) or "auto" (each projection on whichever won
-    # the measured A/B at that size: models/llama.py LlamaModel._PG_AUTO)
+    # the measured A/B at that size: models/llama.py LlamaModel._PG_AUTO - with a shipped
+    # tuned table the library wins every shape the workload reaches, round 5)
     prefill_gemm: str = "auto"
     prefill_gemm_min_rows: int = 128
     # prefill steps of <= 32 rows (cached-prompt planning prefills, short chunks) on the fused

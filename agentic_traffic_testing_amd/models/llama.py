@@ -409,16 +409,22 @@ class LlamaModel:
     # here only when no tuned table is loaded (round 3: 1.06-1.10x over the untuned heuristic at
     # 2600); fp8 gate_up+SiLU 1.08x at 3200, parity at 2048, 0.82-0.92x below; fp8 down
     # 0.89-0.93x (was routed from 2048 in round 3).
-    _PG_AUTO = {(torch.uint8, "gate_up"): 2560}
-    _PG_AUTO_UNTUNED = {(torch.bfloat16, "gate_up"): 2048}
+    # Against the shipped tuned tables the hand-written prefill GEMM wins nowhere that the
+    # workload reaches (round 5, profiles/r5_prefill_gemm_vs_tuned.txt: fp8 gate_up+SiLU
+    # 0.88-0.95x at 2560-3200 rows, bf16 down split-K 0.59-1.03x at 448-1152), so with a table
+    # loaded nothing is routed to it; without one (models with no shipped table) it keeps the
+    # shapes where it beat the untuned library (r3 / r4)
+    _PG_AUTO: dict = {}
+    _PG_AUTO_UNTUNED = {(torch.bfloat16, "gate_up"): 2048, (torch.uint8, "gate_up"): 2560}
     gemm_tuned = False  # set by the model runner when a tuned library table is loaded
     # row ranges where the split-K schedule (co-resident K slices of the few 256 x 256 tiles,
-    # parallel reduction) beat hipBLASLt: bf16 down+residual 1.12-1.15x at M 512 / 1024, parity
-    # at 400 (profiles/r3_prefill_gemm_ab_bf16_splitk.txt)
+    # parallel reduction) beat the UNTUNED hipBLASLt: bf16 down+residual 1.12-1.15x at M 512 /
+    # 1024, parity at 400 (profiles/r3_prefill_gemm_ab_bf16_splitk.txt); not used with a table
     _PG_SPLITK = {(torch.bfloat16, "down"): (448, 1152)}
 
     def _pg_splitk(self, T: int, w: torch.Tensor, proj: str) -> bool:
-        if self.prefill_gemm != "auto" or self.device.type != "cuda" or self.tp_size > 1:
+        if (self.prefill_gemm != "auto" or self.device.type != "cuda" or self.tp_size > 1
+                or self.gemm_tuned):
             return False
         lo, hi = self._PG_SPLITK.get((w.dtype, proj), (1, 0))
         return lo <= T <= hi
