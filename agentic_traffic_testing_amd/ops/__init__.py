@@ -415,6 +415,13 @@ def set_wide_plan(waves: int = 0, ksplit: int = 0) -> None:
     _native().set_wide_plan(int(waves), int(ksplit))
 
 
+def set_wide_min_rows(m: int = 17, m_silu: int = 12) -> None:
+    """Pre-shuffled 16-bit GEMV calls of >= ``m`` rows (gate_up + SiLU: ``m_silu``) run the
+    wide small-M kernel; calls over 32 rows always do.  Defaults = the measured crossover
+    (profiles/r5_wide_vs_skinny.txt); 33 / 33 keeps <= 32 rows on the 16-row-tile GEMVs."""
+    _native().set_wide_min_rows(int(m), int(m_silu))
+
+
 def preshuffle(w: torch.Tensor, rowmap: str = "plain") -> torch.Tensor:
     """Re-lay a [N, K] weight for the decode GEMV: rows permuted into the kernel's tile order
     (``rowmap`` "plain" | "qkv" (RoPE pairs d, d+64 of each 128-dim head in one tile) |

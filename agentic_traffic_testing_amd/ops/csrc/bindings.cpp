@@ -363,6 +363,9 @@ void prefill_gemm_error_to(at::Tensor host, bool clear) {
 void set_wide_plan(int64_t waves, int64_t ksplit) {
   atta_set_wide_plan(static_cast<int>(waves), static_cast<int>(ksplit));
 }
+void set_wide_min_rows(int64_t m, int64_t m_silu) {
+  atta_set_wide_min_rows(static_cast<int>(m), static_cast<int>(m_silu));
+}
 void prefill_gemm_error_reset() {
   check_rc(atta_prefill_gemm_error_reset(), "prefill_gemm_error_reset");
 }
@@ -819,6 +822,7 @@ TORCH_LIBRARY(atta, m) {
   m.def("prefill_gemm_error_to(Tensor(a!) host, bool clear) -> ()", &prefill_gemm_error_to);
   m.def("prefill_gemm_error_reset() -> ()", &prefill_gemm_error_reset);
   m.def("set_wide_plan(int waves, int ksplit) -> ()", &set_wide_plan);
+  m.def("set_wide_min_rows(int m, int m_silu) -> ()", &set_wide_min_rows);
   m.def("prefill_gemm_config(int schedule, int group_m, int ablate=0) -> ()", &prefill_gemm_config);
   m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rms_norm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");

@@ -203,7 +203,20 @@ void atta_set_wide_plan(int waves, int ksplit) {
   g_wide_ksplit = ksplit;
 }
 static int wide(SkinnyParams& p, int epi, int ntiles, int dtype, hipStream_t stream);
-static bool use_wide(int M) { return M > 32; }
+// the wide kernel takes every call over 32 rows and, for pre-shuffled 16-bit weights, calls
+// from g_wide_min_m rows (gate_up + SiLU: g_wide_min_m_silu).  At 17-32 rows the 16-row-tile
+// GEMVs re-read x per weight tile in two row blocks (per layer 120-137 us vs 95-98 us wide);
+// at 12-16 rows only gate_up gains (43.3 / 48.2 -> 39.3 / 39.1 us); at <= 8 rows (decode)
+// the GEMVs win every projection (profiles/r5_wide_vs_skinny.txt)
+static int g_wide_min_m = 17, g_wide_min_m_silu = 12;
+void atta_set_wide_min_rows(int m, int m_silu) {
+  g_wide_min_m = m < 1 ? 1 : m;
+  g_wide_min_m_silu = m_silu < 1 ? 1 : m_silu;
+}
+static bool use_wide(int M, int ps, const float* wscale, bool silu = false) {
+  return M > 32 ||
+         (ps && wscale == nullptr && M >= (silu ? g_wide_min_m_silu : g_wide_min_m));
+}
 
 static int skinny_checks(int M, int K, int waves) {
   if (M < 1 || M > 32) return -1;
@@ -277,7 +290,7 @@ int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual
   p.K = K;
   p.x_stride = x_stride;
   p.eps = 0.f;
-  if (use_wide(M)) {
+  if (use_wide(M, ps, wscale)) {
     if (residual != nullptr && residual != y) return -1;
     p.y = static_cast<uint16_t*>(y);
     p.y_stride = residual != nullptr ? res_stride : y_stride;
@@ -368,7 +381,7 @@ int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x
   p.n_q_heads = n_q_heads;
   p.n_kv_heads = n_kv_heads;
   p.bs_shift = shift;
-  if (use_wide(M)) return wide(p, EPI_QKVROPE, p.N / 16, dtype, stream);
+  if (use_wide(M, ps, wscale)) return wide(p, EPI_QKVROPE, p.N / 16, dtype, stream);
   if (const int rc = setup_split(p, waves, ksplit, p.N / 16, wscale != nullptr)) return rc;
   dim3 grid(p.N / 16, p.ksplit);
   p.wg_trace = take_trace();
@@ -395,7 +408,7 @@ int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int 
   p.N = 2 * inter;
   p.inter = inter;
   p.eps = eps;
-  if (use_wide(M)) return wide(p, EPI_SILU, inter / 8, dtype, stream);
+  if (use_wide(M, ps, wscale, true)) return wide(p, EPI_SILU, inter / 8, dtype, stream);
   if (const int rc = setup_split(p, waves, ksplit, inter / 8, wscale != nullptr)) return rc;
   dim3 grid(inter / 8, p.ksplit);
   p.wg_trace = take_trace();
@@ -411,7 +424,7 @@ int atta_fused_lm_head_sample(int64_t* tokens, unsigned long long* keys, const v
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
   waves = fit_waves(waves, K, wscale != nullptr);
-  const bool wd = use_wide(M) && ps && wscale == nullptr && M <= 128;
+  const bool wd = use_wide(M, ps, wscale) && ps && wscale == nullptr && M <= 128;
   if ((!wd && skinny_checks(M, K, waves)) || N % 16 != 0) return -1;
   SkinnyParams p{};
   p.ps = ps;

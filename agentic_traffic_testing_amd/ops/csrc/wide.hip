@@ -521,6 +521,7 @@ static int launch_reduce_mt(int epi, int mt, const SkinnyParams& p, int ntiles, 
                             int waves, hipStream_t st) {
   switch (mt) {
     case 2: return launch_reduce<T, 2>(epi, p, ntiles, S, waves, st);
+    case 1: return launch_reduce<T, 1>(epi, p, ntiles, S, waves, st);
     case 3: return launch_reduce<T, 3>(epi, p, ntiles, S, waves, st);
     case 4: return launch_reduce<T, 4>(epi, p, ntiles, S, waves, st);
     case 5: return launch_reduce<T, 5>(epi, p, ntiles, S, waves, st);
@@ -593,6 +594,7 @@ static int launch_mt(int epi, int mt, int waves, dim3 grid, hipStream_t st,
                      const SkinnyParams& p, int ntiles) {
   switch (mt) {
     case 2: return launch_w<T, 2>(epi, waves, grid, st, p, ntiles);
+    case 1: return launch_w<T, 1>(epi, waves, grid, st, p, ntiles);
     case 3: return launch_w<T, 3>(epi, waves, grid, st, p, ntiles);
     case 4: return launch_w<T, 4>(epi, waves, grid, st, p, ntiles);
     case 5: return launch_w<T, 5>(epi, waves, grid, st, p, ntiles);
@@ -615,7 +617,7 @@ static void plan(int ntiles, int K, int M, bool norm, int& waves, int& ksplit) {
   const int ws[4] = {4, 6, 7, 8};
   for (int wi = 0; wi < 4; ++wi) {
     const int w = ws[wi];
-    if (norm && !norm_fits(w, M <= 32 ? 2 : (M + 15) / 16)) continue;  // see launch_epi
+    if (norm && !norm_fits(w, (M + 15) / 16)) continue;  // see launch_epi
     const int ncb = (ntiles + w - 1) / w;
     for (int s = 1; s <= 8 && nch / s >= 2; ++s) {
       const double rounds = std::ceil(ncb * s / kCUs);
@@ -652,7 +654,7 @@ int atta_wide_launch(SkinnyParams& p, int epi, int ntiles, int waves, int ksplit
   if (waves != 4 && waves != 6 && waves != 7 && waves != 8) return -1;
   if (ksplit < 1 || p.K / wide::kKC < ksplit) return -1;
   // 16-row blocks: rows padded to the next 16 only (75 rows: 80, not 96)
-  const int mt = p.M <= 32 ? 2 : (p.M + 15) / 16;
+  const int mt = (p.M + 15) / 16;
   const int ncb = (ntiles + waves - 1) / waves;
   // slices' row segments [tile][slice][row][16] + row sums of squares [cb][slice][row]; a
   // split whose slabs do not fit the workspace is halved until they do

@@ -66,6 +66,10 @@ def main():
     ap.add_argument("--plans", action="store_true", help="also sweep (waves, split) plans")
     ap.add_argument("--proj", nargs="+", default=list(SHAPES))
     ap.add_argument("--graph", action="store_true", help="time graph replays (no host cost)")
+    ap.add_argument("--wide-below-33", action="store_true",
+                    help="route <= 32-row calls to the wide kernel too (ops.set_wide_min_rows)")
+    ap.add_argument("--vs-skinny", action="store_true",
+                    help="M <= 32: wide kernel vs the 16-row-tile GEMV (second column)")
     ap.add_argument("--sweep", action="store_true",
                     help="every (waves, split) plan; prints the best per (proj, M)")
     a = ap.parse_args()
@@ -103,8 +107,9 @@ def main():
                                         preshuffled=True)
                 elif proj == "gate_up":
                     ops.decode_gate_up_silu(x, w, 1e-5, out=act, preshuffled=True)
-                else:
-                    ops.linear(x, w, residual=res, preshuffled=True)
+                else:  # as models/llama.py forward_decode calls it
+                    ops.linear(x, w, residual=res, preshuffled=True, ksplit=None, proj=proj,
+                               waves=ops.decode_waves(proj, True, False))
 
             def lib(i):
                 w = raw[i % ncopy]
@@ -116,8 +121,14 @@ def main():
                 else:
                     res.addmm_(x, w.t())
 
+            ops.set_wide_min_rows(*((1, 1) if a.wide_below_33 else (17, 12)))
             tw = timeit(wide)
             tl = timeit(lib)
+            if a.vs_skinny and m <= 32:
+                ops.set_wide_min_rows(33, 33)
+                tl = timeit(wide)  # the "library" column holds the 16-row-tile GEMV here
+                ops.set_wide_min_rows(1, 1)
+                tw = timeit(wide)
             tot.setdefault(m, [0.0, 0.0])
             tot[m][0] += tw
             tot[m][1] += tl

@@ -607,6 +607,14 @@ def test_preshuffled_decode_kernels_bit_identical(m, monkeypatch):
                         {k: {"rm": v["rm"], "ps": v["rm"], "fp8": v["fp8"]}
                          for k, v in ops.DECODE_WAVES.items()})
     monkeypatch.setattr(ops, "DECODE_WAVES_MT2", {})
+    ops.set_wide_min_rows(33, 33)  # 17-32 pre-shuffled rows would run the wide kernel
+    try:
+        _preshuffled_bit_identical(m)
+    finally:
+        ops.set_wide_min_rows()
+
+
+def _preshuffled_bit_identical(m):
     torch.manual_seed(21)
     dt, H, bs = torch.bfloat16, 1024, 16
     x = torch.randn(m, H, dtype=dt, device="cuda")

@@ -1,7 +1,7 @@
-"""Wide small-M GEMM (ops/csrc/wide.hip): 33-128 rows over pre-shuffled 16-bit weights with
+"""Wide small-M GEMM (ops/csrc/wide.hip): 12-128 rows over pre-shuffled 16-bit weights with
 the decode GEMVs' fused epilogues, against the fp32 PyTorch reference (ops/reference.py).
 Every epilogue (plain, residual add, RMSNorm-folded QKV + RoPE + paged K/V write, RMSNorm-
-folded gate_up + SiLU-mul, LM head + sampler keys), ragged M from 33 to 128, and every
+folded gate_up + SiLU-mul, LM head + sampler keys), ragged M from 12 to 128, and every
 (waves, K split) plan the library can pick - split-K slices combined in slice order
 (bitwise deterministic), arrival counters re-armed."""
 import math
@@ -43,7 +43,7 @@ def _norm_ref(x, eps=1e-5):
 @pytest.mark.parametrize("plan", PLANS)
 @pytest.mark.parametrize("m,n,k", [(33, 1024, 4096), (85, 4096, 4096), (128, 512, 14336),
                                    (47, 6144, 1024), (96, 2048, 2048), (75, 4096, 4096),
-                                   (110, 2048, 2048)])
+                                   (110, 2048, 2048), (17, 4096, 4096), (24, 2048, 14336)])
 def test_wide_linear_plain_and_residual(plan, m, n, k):
     torch.manual_seed(41)
     dt = torch.bfloat16
@@ -72,7 +72,7 @@ def test_wide_linear_plain_and_residual(plan, m, n, k):
 
 
 @pytest.mark.parametrize("plan", [(0, 0), (6, 4), (8, 1), (4, 3)])
-@pytest.mark.parametrize("m", [33, 75, 85, 100, 128])
+@pytest.mark.parametrize("m", [20, 33, 75, 85, 100, 128])
 @pytest.mark.parametrize("hq,hkv,H", [(32, 8, 4096), (8, 1, 8192)])
 def test_wide_qkv_rope(plan, m, hq, hkv, H):
     if not _norm_fits(plan[0], m):
@@ -99,7 +99,7 @@ def test_wide_qkv_rope(plan, m, hq, hkv, H):
 
 
 @pytest.mark.parametrize("plan", [(0, 0), (7, 1), (8, 2), (4, 4)])
-@pytest.mark.parametrize("m", [40, 75, 85, 100, 128])
+@pytest.mark.parametrize("m", [12, 16, 27, 40, 75, 85, 100, 128])
 @pytest.mark.parametrize("inter,k", [(14336, 4096), (1792, 8192)])
 def test_wide_gate_up_silu(plan, m, inter, k):
     if not _norm_fits(plan[0], m):
