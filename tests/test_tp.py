@@ -277,6 +277,27 @@ def test_shm_channel_registration_deadline():
         w.publish(np.zeros(1, dtype=np.int32), 0.2)
 
 
+def _check_tp_greedy(m1, got, exp):
+    """TP greedy tokens vs TP=1: the first two tokens equal, and every TP position
+    teacher-forced against the fp32 dense oracle of the same weights: a
+    mismatch must be a near tie (< 0.25 logit) and at most one position in five may differ -
+    random-init weights make late near-tie flips common, so whole-sequence equality with TP=1
+    is not required."""
+    from helpers import dense_logits
+    assert all(g[:2] == e[:2] for g, e in zip(got, exp)), (got, exp)
+    bad_pos = checked = 0
+    for p_, g in zip(_prompts(), got):
+        ids = list(p_)
+        for t in g:
+            lg = dense_logits(m1, ids)
+            checked += 1
+            if int(torch.argmax(lg)) != t:
+                assert float(lg.max() - lg[t]) < 0.25, (g, len(ids) - len(p_))
+                bad_pos += 1
+            ids.append(t)
+    assert bad_pos <= checked // 5, (bad_pos, checked, got, exp)
+
+
 @pytest.mark.gpu
 def test_tp2_same_gpu_rehearsal_host_collectives():
     """Two TP ranks on ONE MI355X with the host-staged gloo collectives (RCCL refuses
@@ -287,6 +308,7 @@ def test_tp2_same_gpu_rehearsal_host_collectives():
     greedy = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
     ref_eng = LLMEngine(EngineConfig(**base))
     exp = [o.token_ids for o in ref_eng.generate(_prompts(), greedy)]
+    m1 = ref_eng.runner.model  # the same seeded weights the TP ranks shard
     del ref_eng
     torch.cuda.empty_cache()
     eng = TPEngine(EngineConfig(tensor_parallel_size=2, tp_same_device=True, **base))
@@ -299,8 +321,7 @@ def test_tp2_same_gpu_rehearsal_host_collectives():
     finally:
         eng.shutdown()
     # bf16 partial sums split across ranks round differently: allow a late near-tie flip
-    assert all(g[:2] == e[:2] for g, e in zip(got, exp)), (got, exp)
-    assert sum(g == e for g, e in zip(got, exp)) >= 2, (got, exp)
+    _check_tp_greedy(m1, got, exp)
 
 
 @pytest.mark.gpu
@@ -312,16 +333,17 @@ def test_tp_same_gpu_graph_captured_decode(tp, model, push):
     collective is an IPC kernel on the peer buffers (X1/X2 sums with the residual add fused
     into the epilogue, X4 sampler-key MAX writing the token ids), so the whole step - every
     rank's 5 kernels x layers + 2 all-reduces per layer + LM head + key MAX - is captured and
-    replayed although the control group is gloo.  Greedy tokens equal TP=1's (graphs on) up to
-    a late bf16 near-tie flip; the IPC timeout word stays 0.  push=True (the default): the o /
-    down GEMVs push their partials straight into the peers' slots (fused push) and one receive
-    kernel per projection adds the sum into the residual; push=False: GEMV + one-shot kernel."""
+    replayed although the control group is gloo.  Greedy tokens: _check_tp_greedy; the IPC
+    timeout word stays 0.  push=True (the default): the o / down GEMVs push their partials
+    straight into the peers' slots (fused push) and one receive kernel per projection adds the
+    sum into the residual; push=False: GEMV + one-shot kernel."""
     base = dict(model=model, device="cuda:0", max_model_len=512, num_kv_blocks=128,
                 max_num_batched_tokens=256, max_num_seqs=4, use_graphs=True)
     greedy = SamplingParams(temperature=0.0, max_tokens=8, ignore_eos=True)
     ref_eng = LLMEngine(EngineConfig(**base))
     exp = [o.token_ids for o in ref_eng.generate(_prompts(), greedy)]
     assert ref_eng.runner.graph_steps > 0
+    m1 = ref_eng.runner.model  # the same seeded weights the TP ranks shard
     del ref_eng
     torch.cuda.empty_cache()
     eng = TPEngine(EngineConfig(tensor_parallel_size=tp, tp_same_device=True,
@@ -342,8 +364,7 @@ def test_tp_same_gpu_graph_captured_decode(tp, model, push):
         assert ipc.check() == 0
     finally:
         eng.shutdown()
-    assert all(g[:2] == e[:2] for g, e in zip(got, exp)), (got, exp)
-    assert sum(g == e for g, e in zip(got, exp)) >= 2, (got, exp)
+    _check_tp_greedy(m1, got, exp)
 
 
 @pytest.mark.gpu
