@@ -37,6 +37,10 @@
 namespace atta {
 namespace wide {
 
+#ifndef ATTA_WIDE_WSTAGES
+#define ATTA_WIDE_WSTAGES 4
+#endif
+constexpr int kDeepW = ATTA_WIDE_WSTAGES;
 constexpr int kKC = 128;             // K columns per staged chunk (4 MFMA K steps)
 constexpr int kRowB = kKC * 2;       // bytes of one staged x row
 constexpr int kSlots = kRowB / 16;   // 16-B slots per staged row
@@ -253,6 +257,7 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
   const int nch = p.K / kKC;
   const int c0 = ks * nch / S, c1 = (ks + 1) * nch / S;
   constexpr bool norm = NORM;  // p.eps > 0: fused RMSNorm (compile-time: no branches in the loop)
+  constexpr int kWStages = kDeepW;  // weight register stages (chunks of weights in flight + 1)
 
   // this wave's weight tile (idle waves of the last column block stream tile 0 and store
   // nothing: every wave takes part in the barriers)
@@ -284,7 +289,7 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
   // computes); x: 2 register sets, chunk j loaded into set (j - c0) % 2 two chunks ahead and
   // written to LDS buffer (j - c0) % 2 one chunk ahead - every wait is for loads issued a full
   // chunk earlier (one chunk ahead exposed the whole load latency at each chunk: 2.2 TB/s)
-  u32x4 w0[4], w1[4], w2[4], xa[PPT], xb[PPT];
+  u32x4 w0[4], w1[4], w2[4], w3[4], xa[PPT], xb[PPT];
   auto load_w = [&](u32x4 (&f)[4], int c) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -332,7 +337,7 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
   auto iter = [&](const u32x4 (&wcur)[4], u32x4 (&wnext)[4], const u32x4 (&xstage)[PPT],
                   u32x4 (&xload)[PPT], int c, int buf) {
     load_x(xload, min(c + 2, clast));
-    load_w(wnext, min(c + 2, clast));
+    load_w(wnext, min(c + kWStages - 1, clast));
     compute(wcur, buf);
     store_x(xstage, buf ^ 1, c + 1 < c1);  // past the end: a re-staged chunk, no squares
     // LDS hand-over only: ds_writes retired, then a bare s_barrier - __syncthreads()' fence
@@ -348,12 +353,31 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
     load_w(w0, c0);
     load_x(xb, min(c0 + 1, clast));
     load_w(w1, min(c0 + 1, clast));
+    if constexpr (kWStages == 4) load_w(w2, min(c0 + 2, clast));
     store_x(xa, 0, true);
   }
   __syncthreads();
+  int c = c0;
+  if constexpr (kWStages == 4) {
+    // whole 4-chunk periods (4 weight stages x 2 x sets: three chunks of weights in flight
+    // while one computes), then the <= 3 remaining chunks
+    for (; c + 4 <= c1; c += 4) {
+      iter(w0, w3, xb, xa, c, 0);
+      iter(w1, w0, xa, xb, c + 1, 1);
+      iter(w2, w1, xb, xa, c + 2, 0);
+      iter(w3, w2, xa, xb, c + 3, 1);
+    }
+    if (c < c1) {
+      iter(w0, w3, xb, xa, c, 0);
+      if (c + 1 < c1) {
+        iter(w1, w0, xa, xb, c + 1, 1);
+        if (c + 2 < c1) iter(w2, w1, xb, xa, c + 2, 0);
+      }
+    }
+    c = c1;
+  }
   // whole 6-chunk periods (3 weight stages x 2 x sets) with no exits inside the loop body, then
   // the <= 5 remaining chunks
-  int c = c0;
   for (; c + 6 <= c1; c += 6) {
     iter(w0, w2, xb, xa, c, 0);
     iter(w1, w0, xa, xb, c + 1, 1);
