@@ -30,7 +30,7 @@ def close(a, b, atol, rtol=0.0):
 
 
 def _norm_fits(waves, m):
-    """Plans built with the RMSNorm fold (wide.hip norm_fits): 6 / 7 waves spill at 113-128
+    """Plans built with the RMSNorm fold (wide.h norm_fits): 6 / 7 waves spill at 113-128
     rows, 6 waves at 97-112."""
     mt = (m + 15) // 16
     return not ((mt == 8 and waves in (6, 7)) or (mt == 7 and waves == 6))
