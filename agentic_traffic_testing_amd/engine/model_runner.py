@@ -141,6 +141,8 @@ class ModelRunner:
             # split-K GEMV workspace up front (32 MiB): a split chosen while a decode graph is
             # being captured (ATTA_DECODE_KSPLIT, TP shards) must not allocate inside the capture
             ops.ensure_splitk_workspace(self.device)
+            if cfg.fused_decode:
+                ops.warm_wide_kernels(self.device, self.dtype)
         self.block_size = cfg.block_size
         self.bt_width = math.ceil(cfg.max_model_len / cfg.block_size)
         self.part_tokens = cfg.decode_partition_tokens

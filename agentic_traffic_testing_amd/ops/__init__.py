@@ -415,6 +415,26 @@ def set_wide_plan(waves: int = 0, ksplit: int = 0) -> None:
     _native().set_wide_plan(int(waves), int(ksplit))
 
 
+def warm_wide_kernels(device, dtype=torch.bfloat16) -> None:
+    """Launch one tiny wide GEMM per 16-row block count (1-8), so every per-block-count code
+    object (ops/csrc/wide_mt<N>.hip) is loaded at engine start: HIP loads a translation unit's
+    code object at the first launch of one of its kernels, which otherwise lands inside a
+    timed prefill (1.5-2.5 ms per object: burst TTFT 4.7 -> 6.3 / 7.3 ms the first time a
+    50 / 95-row burst ran, scripts/gpu/probe_fanout_ttft.py)."""
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        return
+    ensure_splitk_workspace(dev)
+    w = preshuffle(torch.zeros(128, 256, dtype=dtype, device=dev))
+    set_wide_min_rows(1, 1)
+    try:
+        for mt in range(1, 9):
+            linear(torch.zeros(16 * mt, 256, dtype=dtype, device=dev), w, preshuffled=True)
+    finally:
+        set_wide_min_rows()
+    torch.cuda.synchronize(dev)
+
+
 def set_wide_min_rows(m: int = 17, m_silu: int = 12) -> None:
     """Pre-shuffled 16-bit GEMV calls of >= ``m`` rows (gate_up + SiLU: ``m_silu``) run the
     wide small-M kernel; calls over 32 rows always do.  Defaults = the measured crossover

@@ -1,5 +1,7 @@
 // Wide small-M GEMM launcher: plan, split-K reduce launch and the host entry point (the
 // kernel itself: wide.h; one translation unit per 16-row block count: wide_mt<N>.hip).
+#include <cstdlib>
+
 #include "wide.h"
 
 namespace atta {
@@ -119,10 +121,18 @@ int launch_mt_tu(int mt, int epi, int waves, int tpw, dim3 grid, hipStream_t st,
 
 // Grid plan: per candidate (waves, tiles per wave) - T = waves x tpw tiles per workgroup - and
 // K split S <= 8, a time estimate - rounds of the grid over the CUs x (a workgroup's weight
-// bytes + x bytes / 3 at a per-CU streaming rate, plus ~1.5 us of ramp), plus for a split the
+// bytes + x bytes / 6 at a per-CU streaming rate, plus ~1.5 us of ramp), plus for a split the
 // reduce launch - and the cheapest wins.  Slices keep >= 2 chunks of K.
+static double env_or(const char* name, double dflt) {
+  const char* v = std::getenv(name);
+  return v != nullptr ? std::atof(v) : dflt;
+}
+
 static void plan(int ntiles, int K, int M, bool norm, int& waves, int& tpw, int& ksplit) {
   constexpr double kCUs = 256.0, kBpus = 24e3;  // bytes per us per CU
+  // cost-model knobs (env overrides for A/B runs; read once)
+  static const double kXDiv = env_or("ATTA_WIDE_PLAN_XDIV", 6.0);
+  static const double kRed = env_or("ATTA_WIDE_PLAN_RED_US", 1.0);
   const int mpad = ((M + 15) / 16) * 16;
   const int nch = K / kKC;
   double best = 1e30;
@@ -137,12 +147,14 @@ static void plan(int ntiles, int K, int M, bool norm, int& waves, int& tpw, int&
       for (int s = 1; s <= 8 && nch / s >= 2; ++s) {
         const double rounds = std::ceil(ncb * s / kCUs);
         const double kslice = static_cast<double>(K) / s;
-        const double bytes = tb * 16.0 * kslice * 2.0 + mpad * kslice * 2.0 / 3.0;
+        const double bytes = tb * 16.0 * kslice * 2.0 + mpad * kslice * 2.0 / kXDiv;
         const double idle = static_cast<double>(ncb * tb - ntiles) / (ncb * tb);  // empty tiles
-        // split: a reduce launch (~2 us incl. its boundary) reading every slice's slab
+        // split: a reduce launch (~1 us beyond the slabs it reads) reading every slice's slab;
+        // x bytes at 1/6 and the 1 us fitted to the round-5 graph-mode sweep
+        // (profiles/r5_wide_tiles_per_wave_negative.txt: 626 vs 640 us over 20 shapes)
         const double slab = static_cast<double>(ntiles) * s * mpad * 64.0;
         const double t = rounds * (bytes / kBpus * (1.0 + 0.5 * idle) + 1.5) +
-                         (s > 1 ? 2.0 + slab / 5e6 : 0.0);
+                         (s > 1 ? kRed + slab / 5e6 : 0.0);
         if (t < best - 1e-9) {
           best = t;
           waves = w;
