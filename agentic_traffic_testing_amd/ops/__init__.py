@@ -66,6 +66,7 @@ def load_native(build_if_missing: bool = True) -> bool:
         torch.ops.load_library(str(_LIB))
         _loaded = True
         _load_error = None
+        torch.ops.atta.set_flash_waves(FLASH_WAVES)  # the host tiles follow this setting
     except Exception as e:  # pragma: no cover - depends on environment
         _load_error = f"{type(e).__name__}: {e}"
     return _loaded
@@ -222,6 +223,8 @@ PREFILL_IMPL = os.environ.get("ATTA_PREFILL_IMPL", "flash")
 # the flash kernel stages a sequence's whole block-table row in LDS (kBtLds entries: 32k
 # tokens at block size 16); wider tables take the v1 kernel
 FLASH_MAX_BT = 2048
+# waves per flash-prefill workgroup (ops/csrc/flash_prefill.hip NW)
+FLASH_WAVES = int(os.environ.get("ATTA_FLASH_WAVES", "4"))
 
 
 def prefill_impl(bt_width: int = 0, impl: str | None = None) -> str:
@@ -238,11 +241,22 @@ def prefill_impl(bt_width: int = 0, impl: str | None = None) -> str:
 def prefill_tile_tokens(g: int, impl: str | None = None, bt_width: int = 0) -> int:
     """Query tokens per prefill attention workgroup for GQA group ``g``."""
     impl = prefill_impl(bt_width, impl)
-    # 4 waves x (32 // g) tokens (flash: 32 columns per wave) or x (16 // g) (v1: 16) - the
-    # G heads of a token share a wave; G = 3 (Llama-3.2-3B) leaves 2 resp. 1 columns idle
+    # FLASH_WAVES x (32 // g) tokens (flash: 32 columns per wave) or 4 x (16 // g) (v1: 16) -
+    # the G heads of a token share a wave; G = 3 (Llama-3.2-3B) leaves 2 resp. 1 columns idle
     if (impl or PREFILL_IMPL) == "flash":
-        return 4 * (32 // g)
+        return FLASH_WAVES * (32 // g)
     return 4 * (16 // g)
+
+
+def set_flash_waves(nw: int) -> None:
+    """Waves per flash-prefill workgroup (4, or 8: each staged K/V block serves 256 columns).
+    Engines build their prefill tiles from prefill_tile_tokens at start: set this before."""
+    global FLASH_WAVES
+    if nw not in (4, 8):
+        raise ValueError("flash prefill runs 4 or 8 waves per workgroup")
+    FLASH_WAVES = nw
+    if native_available():
+        _native().set_flash_waves(nw)
 
 
 def attention_prefill(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, tile_seq,

@@ -363,6 +363,7 @@ void prefill_gemm_error_to(at::Tensor host, bool clear) {
 void set_wide_plan(int64_t waves, int64_t ksplit) {
   atta_set_wide_plan(static_cast<int>(waves), static_cast<int>(ksplit));
 }
+void set_flash_waves(int64_t nw) { atta_set_flash_waves(static_cast<int>(nw)); }
 void set_wide_min_rows(int64_t m, int64_t m_silu) {
   atta_set_wide_min_rows(static_cast<int>(m), static_cast<int>(m_silu));
 }
@@ -823,6 +824,7 @@ TORCH_LIBRARY(atta, m) {
   m.def("prefill_gemm_error_reset() -> ()", &prefill_gemm_error_reset);
   m.def("set_wide_plan(int waves, int ksplit) -> ()", &set_wide_plan);
   m.def("set_wide_min_rows(int m, int m_silu) -> ()", &set_wide_min_rows);
+  m.def("set_flash_waves(int nw) -> ()", &set_flash_waves);
   m.def("prefill_gemm_config(int schedule, int group_m, int ablate=0) -> ()", &prefill_gemm_config);
   m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rms_norm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");

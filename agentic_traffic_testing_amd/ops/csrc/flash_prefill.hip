@@ -104,12 +104,15 @@ __device__ __forceinline__ float xor32(float v, int idx4) {
   return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(idx4, __builtin_bit_cast(int, v)));
 }
 
-template <typename T, int G>
-__global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
+// NW = 4: every wave stages 16 keys of both K and V; NW = 8 (two workgroup halves): waves
+// 0-3 stage K, waves 4-7 stage V, so each staged K/V block serves 256 columns and a wave issues
+// half the staging instructions.
+template <typename T, int G, int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void flash_prefill_kernel(FlashParams p) {
   using MF = Mf32<T>;
   using frag = typename MF::frag;
   constexpr int kTokPerWave = 32 / G;
-  constexpr int kTokPerWg = 4 * kTokPerWave;
+  constexpr int kTokPerWg = NW * kTokPerWave;
   __shared__ __attribute__((aligned(16))) uint16_t lds_k[2][kKTile];
   __shared__ __attribute__((aligned(16))) uint16_t lds_v[2][kVTile];
   __shared__ int lds_bt[kBtLds];
@@ -154,7 +157,7 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
 
   // ---- block table slice -> LDS -------------------------------------------------------
   const int npages = min((wg_end + BS - 1) >> p.bs_shift, kBtLds);
-  for (int i = tid; i < npages; i += 256) lds_bt[i] = bt[i];
+  for (int i = tid; i < npages; i += NW * 64) lds_bt[i] = bt[i];
 
   // ---- Q (B operand): Q[col r][16 st + 8 h .. +8], 8 k-steps over D ----------------------
   frag qf[8];
@@ -180,11 +183,16 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
   static_assert(kKB == 64 && kChunks == 4, "wave w stages keys 16 w .. 16 w + 15");
   const int pshift = p.bs_shift + 7;        // log2(BS * kD) elements per (page, head)
   const int last_page = npages - 1;
-  const int w_keyoff = (16 * wid) & (BS - 1);               // wave's first key in its page
+  // staging key group of this wave (16 keys) and which tensors it stages
+  const int sg = NW == 8 ? (wid & 3) : wid;
+  constexpr bool kBoth = NW == 4;
+  const bool stage_k = kBoth || wid < 4;
+  const bool stage_v = kBoth || wid >= 4;
+  const int w_keyoff = (16 * sg) & (BS - 1);                // group's first key in its page
   const int k_lane = (lane >> 4) * kD + 8 * (lane & 15) + w_keyoff * kD;
   const int v_lane = (lane >> 1) * BS + 8 * (lane & 1) + w_keyoff;
-  const int k_lds = (16 * wid + (lane >> 4)) * kKStride + 8 * (lane & 15);
-  const int v_lds = (lane >> 1) * kVStride + 16 * wid + 4 * (lane & 1);  // permuted: see kVStride
+  const int k_lds = (16 * sg + (lane >> 4)) * kKStride + 8 * (lane & 15);
+  const int v_lds = (lane >> 1) * kVStride + 16 * sg + 4 * (lane & 1);  // permuted: see kVStride
   // LDS only (the launcher rejects bt_stride > kBtLds): a select between the LDS copy and the
   // global table compiled to FLAT loads, whose vmcnt wait put a dependent global round trip
   // in front of every block's K/V loads.  Keys past the workgroup's range (>= wg_end) read a
@@ -192,27 +200,39 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
   // held that page before.  Their scores are masked (P = 0), and their V^T columns are zeroed
   // at staging (store_block), so a non-finite stale value cannot turn 0 * V into NaN
   // (no invariant on the cache contents is needed).
-  u32x4 kr[kChunks], vr[kChunks];
+  u32x4 kr[kBoth ? kChunks : 1], vr[kChunks];  // NW = 8: one register set (vr) per wave
   auto load_block = [&](int kb) {
-    const int pi = min((kb * kKB + 16 * wid) >> p.bs_shift, last_page);
+    const int pi = min((kb * kKB + 16 * sg) >> p.bs_shift, last_page);
     const int pg = __builtin_amdgcn_readfirstlane(lds_bt[pi]);
     const uint64_t off = static_cast<uint64_t>(static_cast<uint32_t>(pg * p.n_kv_heads + hk)) << pshift;
     const uint16_t* kb_ = p.k_cache + off;
     const uint16_t* vb_ = p.v_cache + off;
+    if constexpr (kBoth) {
 #pragma unroll
-    for (int u = 0; u < kChunks; ++u)
-      kr[u] = *reinterpret_cast<const u32x4*>(kb_ + k_lane + u * 4 * kD);
+      for (int u = 0; u < kChunks; ++u)
+        kr[u] = *reinterpret_cast<const u32x4*>(kb_ + k_lane + u * 4 * kD);
 #pragma unroll
-    for (int u = 0; u < kChunks; ++u)
-      vr[u] = *reinterpret_cast<const u32x4*>(vb_ + v_lane + u * 32 * BS);
+      for (int u = 0; u < kChunks; ++u)
+        vr[u] = *reinterpret_cast<const u32x4*>(vb_ + v_lane + u * 32 * BS);
+    } else {
+      // wave-uniform choice of tensor; the same registers carry K rows or V rows
+#pragma unroll
+      for (int u = 0; u < kChunks; ++u)
+        vr[u] = stage_k ? *reinterpret_cast<const u32x4*>(kb_ + k_lane + u * 4 * kD)
+                        : *reinterpret_cast<const u32x4*>(vb_ + v_lane + u * 32 * BS);
+    }
   };
   auto store_block = [&](int buf, int kb) {
+    if (stage_k) {
 #pragma unroll
-    for (int u = 0; u < kChunks; ++u)
-      *reinterpret_cast<u32x4*>(&lds_k[buf][k_lds + u * 4 * kKStride]) = kr[u];
-    // this lane's 8 V keys: kb * kKB + 16 wid + 8 (lane & 1) + j; only the last block can
+      for (int u = 0; u < kChunks; ++u)
+        *reinterpret_cast<u32x4*>(&lds_k[buf][k_lds + u * 4 * kKStride]) =
+            kBoth ? kr[kBoth ? u : 0] : vr[u];
+    }
+    if (!stage_v) return;
+    // this lane's 8 V keys: kb * kKB + 16 sg + 8 (lane & 1) + j; only the last block can
     // reach past wg_end (uniform per workgroup except at that edge)
-    const int vkey = kb * kKB + 16 * wid + 8 * (lane & 1);
+    const int vkey = kb * kKB + 16 * sg + 8 * (lane & 1);
     if (vkey + 8 > wg_end) {
 #pragma unroll
       for (int u = 0; u < kChunks; ++u)
@@ -373,22 +393,33 @@ __global__ __launch_bounds__(256, 2) void flash_prefill_kernel(FlashParams p) {
   }
 }
 
-template <typename T>
-static int launch(int G, dim3 grid, hipStream_t st, const FlashParams& p) {
+template <typename T, int NW>
+static int launch_nw(int G, dim3 grid, hipStream_t st, const FlashParams& p) {
   switch (G) {
-    case 1: flash_prefill_kernel<T, 1><<<grid, 256, 0, st>>>(p); return 0;
-    case 2: flash_prefill_kernel<T, 2><<<grid, 256, 0, st>>>(p); return 0;
-    case 3: flash_prefill_kernel<T, 3><<<grid, 256, 0, st>>>(p); return 0;
-    case 4: flash_prefill_kernel<T, 4><<<grid, 256, 0, st>>>(p); return 0;
-    case 8: flash_prefill_kernel<T, 8><<<grid, 256, 0, st>>>(p); return 0;
+    case 1: flash_prefill_kernel<T, 1, NW><<<grid, NW * 64, 0, st>>>(p); return 0;
+    case 2: flash_prefill_kernel<T, 2, NW><<<grid, NW * 64, 0, st>>>(p); return 0;
+    case 3: flash_prefill_kernel<T, 3, NW><<<grid, NW * 64, 0, st>>>(p); return 0;
+    case 4: flash_prefill_kernel<T, 4, NW><<<grid, NW * 64, 0, st>>>(p); return 0;
+    case 8: flash_prefill_kernel<T, 8, NW><<<grid, NW * 64, 0, st>>>(p); return 0;
     default: return -1;
   }
+}
+
+// waves per workgroup (4 or 8); the host's tiles must hold NW * (32 / G) tokens
+// (ops.prefill_tile_tokens reads the same setting)
+static int g_flash_waves = 4;
+
+template <typename T>
+static int launch(int G, dim3 grid, hipStream_t st, const FlashParams& p) {
+  return g_flash_waves == 8 ? launch_nw<T, 8>(G, grid, st, p) : launch_nw<T, 4>(G, grid, st, p);
 }
 
 }  // namespace fp
 }  // namespace atta
 
 using namespace atta;
+
+void atta_set_flash_waves(int nw) { fp::g_flash_waves = nw == 8 ? 8 : 4; }
 
 int atta_flash_prefill(void* out, const void* q, const void* k_cache, const void* v_cache,
                        const int* block_tables, const int* seq_kvlen, const int* seq_qstart,

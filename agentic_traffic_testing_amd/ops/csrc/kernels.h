@@ -151,4 +151,5 @@ int atta_prefill_gemm_error_async(void* host, hipStream_t stream, int clear);
 int atta_prefill_gemm_error_reset();
 void atta_set_wide_plan(int waves, int ksplit);
 void atta_set_wide_min_rows(int m, int m_silu);
+void atta_set_flash_waves(int nw);
 int atta_prefill_gemm_config(int schedule, int group_m, int ablate);
