@@ -1,33 +1,35 @@
-// Wide small-M GEMM: 33 <= M <= 128 rows over pre-shuffled 16-bit weights, with the decode
-// GEMVs' fused epilogues (skinny.h tile_epilogue: residual add, RMSNorm fold + RoPE + paged
-// K/V write, SiLU-mul, LM-head sampler keys).  Serves the prefix-cached burst prefill (the
-// headline's ~85-row burst, reference agents/agent_a/server.py:534-623) and decode batches of
-// 33-128 sequences (reference llm/serve_llm.py:362-373 max_num_seqs), which the 16-row-tile
-// GEMV (gemv.hip) serves badly: it re-reads every x row from L2 once per 16 weight rows in
-// fragment-shaped 16 x 64-B pieces - at 32 rows gate_up streamed 2.9 TB/s
-// (profiles/r4_skinny_mt_probe.txt).
+// Wide small-M GEMM: 1 <= M <= 128 rows (routed from 17 rows, gate_up + SiLU from 12:
+// gemv.hip use_wide) over pre-shuffled 16-bit weights, with the decode GEMVs' fused epilogues
+// (residual add, RMSNorm fold + RoPE + paged K/V write, SiLU-mul, LM-head sampler keys).
+// Serves the prefix-cached burst and planning prefills (the headline's 50-105-row bursts,
+// reference agents/agent_a/server.py:534-623) and decode batches of 17-128 sequences
+// (reference llm/serve_llm.py:362-373 max_num_seqs), which the 16-row-tile GEMV (gemv.hip)
+// serves badly: it re-reads every x row from L2 once per 16 weight rows in fragment-shaped
+// 16 x 64-B pieces - at 32 rows gate_up streamed 2.9 TB/s (profiles/r4_skinny_mt_probe.txt).
 //
-// Decomposition.  A workgroup owns WAVES consecutive 16-column weight tiles (wave w: tile
-// cb * WAVES + w) over one K slice (split-K S = gridDim.y, for the narrow projections so the
-// grid covers the 256 CUs), and all M rows:
+// Decomposition.  A workgroup owns WAVES x TPW consecutive 16-column weight tiles (wave w:
+// tiles cb * WAVES * TPW + w * TPW + j; only TPW = 1 is built: two tiles per wave measured
+// slower) over one K slice (split-K S = gridDim.y, for the narrow projections so the grid
+// covers the 256 CUs), and all M rows in MT = ceil(M / 16) 16-row blocks:
 //   * x is staged ONCE per workgroup through LDS in 128-column chunks (M_pad x 256 B, full
 //     128-B lines, plain 16-B loads into registers then ds_write_b128 into an XOR-swizzled
 //     image - slot j of row r at slot j ^ (r & 15): every ds_read_b128 lane group of the
-//     fragment reads is conflict-free) and read by all WAVES waves: x's L2 traffic is
+//     fragment reads is conflict-free) and read by all waves: x's L2 traffic is
 //     M / (16 WAVES) of the weight bytes instead of M / 16;
 //   * each wave streams its tile's pre-shuffled weights (one contiguous 1 KiB per 32-wide K
-//     step) straight to VGPRs, two 4-step chunks ahead, non-temporal;
+//     step) straight to VGPRs, three 4-step chunks ahead (4 register stages), non-temporal;
 //   * per K step a wave applies its weight fragment (MFMA B operand) to all MT 16-row x
 //     fragments (A operand, ds_read_b128) - the weights are read once for every row;
 //   * the RMSNorm fold needs sum(x^2) per row: accumulated from the staged x registers;
 //   * split-K: each slice writes its fp32 row segments and partial sums of squares with
-//     plain stores and exits; a second launch (wide_reduce_kernel, one wave per tile) sums
-//     them in slice order - bitwise deterministic - and runs the epilogue.  (An in-launch
-//     last-arriver combine read every slice of a column block from ONE workgroup: 5-17 us
-//     at 85 rows against a 1.5 us launch boundary.)
+//     plain stores and exits; a second launch (wide.hip wide_reduce_kernel, one wave per
+//     (tile, 16-row group)) sums them in slice order - bitwise deterministic - and runs the
+//     epilogue.  (In-launch hand-overs measured slower: one last arriver reading every slice
+//     5-17 us at 85 rows; every slice reducing 1/S after a counter wait 7-17 us.)
 // One workgroup barrier per chunk.  Plain loads only (no LDS-DMA): mixing LDS-DMA with the
 // register weight stream makes hipcc wait vmcnt(0) at every weight use (cdna_hip_programming
-// §5, "Projection GEMM at M = 256" item 4(b)).
+// §5, "Projection GEMM at M = 256" item 4(b)).  Compiled one 16-row block count per
+// translation unit (wide_mt<N>.hip) so the build runs them in parallel.
 #pragma once
 #include <cmath>
 
