@@ -180,6 +180,7 @@ int atta_wide_launch(SkinnyParams& p, int epi, int ntiles, int waves, int ksplit
                      hipStream_t stream) {
   if (p.M < 1 || p.M > 128 || p.K % wide::kKC != 0 || !p.ps || p.wscale != nullptr) return -1;
   // waves 14 / 16 / 17 / 18 in an explicit plan = 4 / 6 / 7 / 8 waves x two tiles per wave
+  // (measured slower and not built: such a plan returns -1 from the launcher)
   int tpw = 1;
   if (waves > 10) {
     tpw = 2;
