@@ -17,6 +17,8 @@
 // workspace with device-scope stores and arrives on a per-(seq, kv-head) counter; the last
 // arriver reads every partition back with device-scope loads, merges them and writes the
 // bf16 output, then re-arms the counter (counters are zeroed once at allocation).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -384,13 +386,28 @@ static int launch_g(int G, dim3 grid, hipStream_t st, const DecParams& p) {
   }
 }
 
-// part_tokens selects the workgroup shape: 64 = 4 waves x 1 tile, 128 = 4 waves x 2 tiles,
-// 256 = 8 x 2, 512 = 16 x 2 (16 waves cap VGPRs at 128: more tiles per wave would spill).
+// part_tokens selects the workgroup shape: 64 = 4 waves x 1 tile, 128 = 8 waves x 1 tile (or
+// 4 x 2, attn128_waves), 256 = 8 x 2, 512 = 16 x 2 (16 waves cap VGPRs at 128: more tiles per
+// wave would spill).
+// 128-token partitions (the decode batches <= 8 of the headline) run as 8 waves x 1 tile:
+// half the serial QK / softmax / PV chain per wave and twice the waves in flight against
+// 4 waves x 2 tiles - bench 767.9 / 769.2 vs 762.4 / 764.0 tok/s interleaved on one box
+// (profiles/r5_attention_8wave.txt).  ATTA_ATTN128_WAVES=4 restores 4 x 2 (read once).
+static int attn128_waves() {
+  static const int w = [] {
+    const char* v = std::getenv("ATTA_ATTN128_WAVES");
+    return v != nullptr && std::atoi(v) == 4 ? 4 : 8;
+  }();
+  return w;
+}
+
 template <typename T>
 static int launch(int G, int part_tokens, dim3 grid, hipStream_t st, const DecParams& p) {
   switch (part_tokens) {
     case 64: return launch_g<T, 4, 1>(G, grid, st, p);
-    case 128: return launch_g<T, 4, 2>(G, grid, st, p);
+    case 128:
+      return attn128_waves() == 8 ? launch_g<T, 8, 1>(G, grid, st, p)
+                                  : launch_g<T, 4, 2>(G, grid, st, p);
     case 256: return launch_g<T, 8, 2>(G, grid, st, p);
     case 512: return launch_g<T, 16, 2>(G, grid, st, p);
     default: return -1;
