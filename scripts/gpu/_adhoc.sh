@@ -1,11 +1,9 @@
 set -o pipefail
 set -e
-ATTA_ATTN256_WAVES=16 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_kernels_gpu.py -k "decode" > gpurun_out/r5_attn16_tests.log 2>&1 || { tail -20 gpurun_out/r5_attn16_tests.log; exit 1; }
-tail -1 gpurun_out/r5_attn16_tests.log
-PT=256 CTXS="600;450,450,450,450,450;900,900,900,900,900;3500" ATTA_ATTN256_WAVES=16 timeout -k 10 300 python -u scripts/gpu/trace_decode_attention.py > gpurun_out/attn256_w16.txt 2>&1
-PT=128 CTXS="600;450,450,450,450,450;900,900,900,900,900;3500" timeout -k 10 300 python -u scripts/gpu/trace_decode_attention.py > gpurun_out/attn128_w8b.txt 2>&1
-paste -d'|' gpurun_out/attn128_w8b.txt gpurun_out/attn256_w16.txt | grep -v amdgpu | cut -c1-200
-for i in 1 2; do for v in 128 256; do
-ATTA_ATTN256_WAVES=16 timeout -k 10 600 python -u bench.py --steps 3 --warmup 2 --set decode_partition_tokens_small=$v > gpurun_out/r5_pt${v}_$i.log 2>&1
-python -c "import json; d=json.loads(open('gpurun_out/r5_pt${v}_$i.log').read().strip().splitlines()[-1]); print('small partitions $v', d['value'], d['p50_ttft_s'])"
-done; done
+export PYTHONUNBUFFERED=1
+for w in 4 8; do
+ATTA_ATTN128_WAVES=$w timeout -k 10 300 python -u -m pytest tests/test_engine.py -k fp8_engine_matches_fp32_oracle -m gpu -q -s -p no:cacheprovider --timeout 150 --timeout-method thread > gpurun_out/r5_fp8oracle_w$w.log 2>&1 || true
+echo "waves $w"; grep -E "fp8 oracle|passed|failed" gpurun_out/r5_fp8oracle_w$w.log
+done
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 150 --timeout-method thread > gpurun_out/r5_gpu_tier_final2.log 2>&1 || { tail -40 gpurun_out/r5_gpu_tier_final2.log; exit 1; }
+tail -3 gpurun_out/r5_gpu_tier_final2.log
