@@ -1,9 +1,11 @@
 set -o pipefail
 set -e
 export PYTHONUNBUFFERED=1
-for w in 4 8; do
-ATTA_ATTN128_WAVES=$w timeout -k 10 300 python -u -m pytest tests/test_engine.py -k fp8_engine_matches_fp32_oracle -m gpu -q -s -p no:cacheprovider --timeout 150 --timeout-method thread > gpurun_out/r5_fp8oracle_w$w.log 2>&1 || true
-echo "waves $w"; grep -E "fp8 oracle|passed|failed" gpurun_out/r5_fp8oracle_w$w.log
-done
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 150 --timeout-method thread > gpurun_out/r5_gpu_tier_final2.log 2>&1 || { tail -40 gpurun_out/r5_gpu_tier_final2.log; exit 1; }
-tail -3 gpurun_out/r5_gpu_tier_final2.log
+timeout -k 10 400 python -u -m pytest tests/test_wide_gemm.py -x -q -p no:cacheprovider --timeout 150 --timeout-method thread > gpurun_out/r5_ks_tests.log 2>&1 || { tail -30 gpurun_out/r5_ks_tests.log; exit 1; }
+tail -1 gpurun_out/r5_ks_tests.log
+timeout -k 10 400 python -u scripts/gpu/bench_wide.py --graph --plans --proj o down --m 33 50 75 85 95 105 128 > gpurun_out/r5_ks_bench_wide.txt 2>&1
+cat gpurun_out/r5_ks_bench_wide.txt | grep -v amdgpu
+for i in 1 2; do for v in 0 1; do
+ATTA_WIDE_KS=$v timeout -k 10 600 python -u bench.py --steps 3 --warmup 2 > gpurun_out/r5_ks${v}_$i.log 2>&1
+python -c "import json; d=json.loads(open('gpurun_out/r5_ks${v}_$i.log').read().strip().splitlines()[-1]); print('KS $v', d['value'], d['p50_ttft_s'], d['ttft_by_phase'])"
+done; done
