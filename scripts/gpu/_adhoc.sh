@@ -1,7 +1,6 @@
 set -o pipefail
 set -e
 export PYTHONUNBUFFERED=1
-for i in 1 2; do for v in "0,0" "49,120" "33,120"; do
-ATTA_O_LIBRARY_ROWS=$v timeout -k 10 600 python -u scripts/gpu/probe_fanout_ttft.py --episodes 4 --warmup 5 > gpurun_out/r5_olib_${v/,/_}_$i.log 2>&1
-echo "o-library rows $v"; grep -E "burst|planning" gpurun_out/r5_olib_${v/,/_}_$i.log | awk '{printf "%s %d %s; ", $3, $5-$7, $10}'; echo
-done; done
+export ATTA_GRAPH_META_COPY=1
+PROF_NAME=r5prof_gaps_gcopy STEPS=1 WARMUP=1 bash scripts/gpu/profile_bench.sh > gpurun_out/r5prof_gaps_gcopy_run.txt 2>&1 || { tail -20 gpurun_out/r5prof_gaps_gcopy_run.txt; exit 1; }
+sed -n '/wall span/,$p' gpurun_out/r5prof_gaps_gcopy_summary.txt

@@ -67,3 +67,36 @@ if gaps:
     for k, v in sorted(gaps.items(), key=lambda kv: -len(kv[1])):
         v.sort()
         print(f"  {k:50s} {len(v):7d} {statistics.median(v):7.2f} {v[int(0.9 * (len(v) - 1))]:7.2f}")
+
+# Where the GPU idles: every gap between consecutive dispatches (any kernels), by size bucket,
+# and the kernel pairs that hold the most idle time in total.
+def pair_name(n):
+    k = short_name(n)
+    if k:
+        return k
+    for key in ("embed_kernel", "wide_kernel", "wide_reduce", "flash_prefill", "rms_norm",
+                "rope_cache", "Cijk", "copyBuffer", "fillBuffer", "stream_read"):
+        if key in n:
+            return key
+    return n[:40]
+
+
+if len(rows) > 1:
+    buckets = [(5, "<5us"), (20, "5-20us"), (100, "20-100us"), (1000, "0.1-1ms"),
+               (float("inf"), ">1ms")]
+    bsum = defaultdict(float); bcnt = defaultdict(int)
+    psum = defaultdict(float); pcnt = defaultdict(int)
+    for (s0, e0, n0), (s1, e1, n1) in zip(rows, rows[1:]):
+        g = (s1 - e0) / 1e3
+        if g <= 0:
+            continue
+        lab = next(lab for lim, lab in buckets if g < lim)
+        bsum[lab] += g; bcnt[lab] += 1
+        key = f"{pair_name(n0)} -> {pair_name(n1)}"
+        psum[key] += g; pcnt[key] += 1
+    print("\nidle gaps between consecutive dispatches: bucket, count, total ms")
+    for _, lab in buckets:
+        print(f"  {lab:10s} {bcnt[lab]:8d} {bsum[lab] / 1e3:9.2f}")
+    print("kernel pairs holding the most idle time: pair, count, total ms, mean us")
+    for k, v in sorted(psum.items(), key=lambda kv: -kv[1])[:15]:
+        print(f"  {k:60s} {pcnt[k]:7d} {v / 1e3:8.2f} {v / pcnt[k]:8.1f}")
