@@ -1,10 +1,9 @@
 set -o pipefail
-export PYTHONUNBUFFERED=1
-run() {  # tag, env assignments...
-  local tag=$1; shift
-  env "$@" timeout -k 10 300 python bench.py --steps 3 --warmup 2 > gpurun_out/sweep5b_$tag.log 2>&1 || return 1
-  echo "$tag $* $(grep -o '"value": [0-9.]*' gpurun_out/sweep5b_$tag.log)"
-}
-run base_a ATTA_X=0 && run lm8_a ATTA_DECODE_WAVES=lm_head.ps=8 &&
-run base_b ATTA_X=0 && run lm8_b ATTA_DECODE_WAVES=lm_head.ps=8 &&
-run base_c ATTA_X=0 && run lm8_c ATTA_DECODE_WAVES=lm_head.ps=8
+set -e
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+OUT=gpurun_out/r5prof_burst
+rm -rf $OUT; mkdir -p $OUT
+timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d $OUT -o run -- python3 bench.py --steps 2 --warmup 5 > gpurun_out/r5prof_burst_bench.log 2>&1
+for k in 0 1 2 3; do python3 scripts/gpu/step_breakdown.py $OUT --mt-min 3 --nth $k; done > gpurun_out/r5_burst_breakdown.txt 2>&1
+cat gpurun_out/r5_burst_breakdown.txt
+find $OUT -name "*kernel_trace.csv" -delete
