@@ -1,9 +1,7 @@
 set -o pipefail
 set -e
-export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-OUT=gpurun_out/r5prof_burst
-rm -rf $OUT; mkdir -p $OUT
-timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d $OUT -o run -- python3 bench.py --steps 2 --warmup 5 > gpurun_out/r5prof_burst_bench.log 2>&1
-for k in 0 1 2 3; do python3 scripts/gpu/step_breakdown.py $OUT --mt-min 3 --nth $k; done > gpurun_out/r5_burst_breakdown.txt 2>&1
-cat gpurun_out/r5_burst_breakdown.txt
-find $OUT -name "*kernel_trace.csv" -delete
+export PYTHONUNBUFFERED=1
+for i in 1 2; do for v in 4 8; do
+ATTA_FLASH_WAVES=$v timeout -k 10 600 python -u scripts/gpu/probe_fanout_ttft.py --episodes 4 --warmup 5 > gpurun_out/r5_fw${v}_$i.log 2>&1
+echo "flash waves $v"; grep -E "burst|planning|final" gpurun_out/r5_fw${v}_$i.log | awk '{printf "%s %d %s; ", $3, $5-$7, $10}'; echo
+done; done
