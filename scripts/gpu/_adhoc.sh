@@ -1,7 +1,7 @@
 set -o pipefail
 set -e
 export PYTHONUNBUFFERED=1
-for i in 1 2; do for v in 4 8; do
-ATTA_FLASH_WAVES=$v timeout -k 10 600 python -u scripts/gpu/probe_fanout_ttft.py --episodes 4 --warmup 5 > gpurun_out/r5_fw${v}_$i.log 2>&1
-echo "flash waves $v"; grep -E "burst|planning|final" gpurun_out/r5_fw${v}_$i.log | awk '{printf "%s %d %s; ", $3, $5-$7, $10}'; echo
-done; done
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r5_smoke_final3.log 2>&1
+grep -v amdgpu gpurun_out/r5_smoke_final3.log | tail -1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 150 --timeout-method thread > gpurun_out/r5_gpu_tier_final3.log 2>&1 || { tail -40 gpurun_out/r5_gpu_tier_final3.log; exit 1; }
+tail -1 gpurun_out/r5_gpu_tier_final3.log
