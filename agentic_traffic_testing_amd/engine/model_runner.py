@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import math
 import os
+import threading
 import time
 
 import numpy as np
@@ -205,6 +206,8 @@ class ModelRunner:
         # on every read), and how many steps ever reported one
         self.kernel_error = 0
         self.kernel_error_steps = 0
+        # the engine thread ORs words in, the HTTP loop's /health swaps them out
+        self._kernel_error_lock = threading.Lock()
         self._last_collect = 0.0
         nkv = self.model.n_kv_heads
         self.part_out = torch.empty(self.max_seqs * nkv * alloc_parts * 16 * 128,
@@ -494,8 +497,9 @@ class ModelRunner:
         word = int(self._err_host[0]) if self.is_cuda else 0
         if word:
             self._err_host.zero_()
-            self.kernel_error |= word
-            self.kernel_error_steps += 1
+            with self._kernel_error_lock:
+                self.kernel_error |= word
+                self.kernel_error_steps += 1
             print(f"[model_runner] prefill GEMM error word {word:#x}: a "
                   "cross-workgroup wait timed out (tiles recomputed, outputs exact; the GPU "
                   "is shared or oversubscribed)", flush=True)
@@ -503,7 +507,8 @@ class ModelRunner:
 
     def take_kernel_error(self) -> int:
         """Error words seen since the previous call (the /health check), then cleared."""
-        w, self.kernel_error = self.kernel_error, 0
+        with self._kernel_error_lock:
+            w, self.kernel_error = self.kernel_error, 0
         return w
 
     def launchable(self, batch: Batch) -> bool:

@@ -484,9 +484,9 @@ class LlamaModel:
 
     def decode_fusable(self, num_tokens: int) -> bool:
         """Can a step of this many rows run the fused weight-streaming kernels?  <= 32 rows:
-        the 16-row-tile GEMVs (any layout); 33..WIDE_MAX_M rows: the wide small-M kernel,
-        which needs the pre-shuffled 16-bit weights (TP=1: the TP decode step's push /
-        one-shot collectives are sized for <= 32 rows)."""
+        the 16-row-tile GEMVs (any layout); 33..128 rows: the wide small-M kernel; 129..
+        ops.MIDM_MAX_M rows: the mid-M kernel - both over the pre-shuffled 16-bit weights
+        (TP=1: the TP decode step's push / one-shot collectives are sized for <= 32 rows)."""
         # 16-bit GEMVs: K % 128 (4 waves x 32); fp8 GEMVs: K % 256 (4 waves x 64)
         step = 256 if self.quant == "fp8" else 128
         dims = (self.device.type == "cuda" and self.cfg.hidden_size % step == 0
@@ -495,7 +495,8 @@ class LlamaModel:
             return False
         if num_tokens <= ops.SKINNY_MAX_M:
             return True
-        return (num_tokens <= ops.WIDE_MAX_M and self.quant != "fp8" and self.tp_size == 1
+        return (num_tokens <= ops.fused_max_rows(True, self.quant == "fp8")
+                and self.quant != "fp8" and self.tp_size == 1
                 and bool(self.layers) and self.layers[0].qkv_ps is not None
                 and self.lm_head_ps is not None)
 

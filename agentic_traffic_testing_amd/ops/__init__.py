@@ -67,6 +67,8 @@ def load_native(build_if_missing: bool = True) -> bool:
         _loaded = True
         _load_error = None
         torch.ops.atta.set_flash_waves(FLASH_WAVES)  # the host tiles follow this setting
+        if WIDE_MAX_M <= SKINNY_MAX_M:  # wide kernel off: no <= 32-row call may take it
+            torch.ops.atta.set_wide_min_rows(33, 33)
     except Exception as e:  # pragma: no cover - depends on environment
         _load_error = f"{type(e).__name__}: {e}"
     return _loaded
@@ -225,6 +227,8 @@ PREFILL_IMPL = os.environ.get("ATTA_PREFILL_IMPL", "flash")
 FLASH_MAX_BT = 2048
 # waves per flash-prefill workgroup (ops/csrc/flash_prefill.hip NW)
 FLASH_WAVES = int(os.environ.get("ATTA_FLASH_WAVES", "4"))
+if FLASH_WAVES not in (4, 8):  # the host tiles must match what the kernel covers
+    raise ValueError(f"ATTA_FLASH_WAVES={FLASH_WAVES}: flash prefill runs 4 or 8 waves")
 
 
 def prefill_impl(bt_width: int = 0, impl: str | None = None) -> str:
@@ -326,8 +330,24 @@ SKINNY_MAX_M = int(os.environ.get("ATTA_SKINNY_MAX_M", "32"))
 # 33..WIDE_MAX_M rows over PRE-SHUFFLED 16-bit weights run the wide small-M kernel
 # (csrc/wide.hip: x staged once per workgroup in LDS and shared by its tiles, split-K for the
 # narrow projections), with the same fused epilogues - burst prefills and decode batches of
-# up to 128 sequences.  0 turns it off.
+# up to 128 sequences.  0 (or anything <= SKINNY_MAX_M) turns it off.
 WIDE_MAX_M = int(os.environ.get("ATTA_WIDE_MAX_M", "128"))
+# 129..MIDM_MAX_M rows over pre-shuffled 16-bit weights run the mid-M kernel (csrc/midm.h:
+# row-blocked BM x 128 tiles, ~256 workgroups, the same fused epilogues) - the uncached burst
+# and planning prefills.  Needs the wide kernel on up to 128 rows; 0 turns it off.
+MIDM_MAX_M = int(os.environ.get("ATTA_MIDM_MAX_M", "1024"))
+
+
+def fused_max_rows(preshuffled: bool = True, fp8: bool = False) -> int:
+    """Most rows a call may have to run on the hand-written weight-streaming kernels (the
+    16-row-tile GEMVs, the wide small-M kernel, the mid-M kernel) for this weight format."""
+    if not preshuffled or fp8 or WIDE_MAX_M <= SKINNY_MAX_M:
+        return SKINNY_MAX_M
+    if WIDE_MAX_M >= 128 and MIDM_MAX_M > 128:
+        return MIDM_MAX_M
+    return min(WIDE_MAX_M, 128)
+
+
 SKINNY_WAVES = int(os.environ.get("ATTA_SKINNY_WAVES", "8"))
 # per-projection wave counts from the MI355X sweep (profiles/r1_microbench_v3_plain.txt):
 # 8 waves x 2-deep stages for the small qkv / o projections, 16 waves for the large ones.
@@ -383,7 +403,7 @@ def auto_ksplit(tiles: int, K: int) -> int:
         ks *= 2
     return ks
 
-SPLITK_WS_FLOATS = 8 << 20   # 32 MiB: tiles x split x (32 x 16 + 32) fp32 slots
+SPLITK_WS_FLOATS = 16 << 20  # 64 MiB: tiles x split x rows x 16 fp32 slots (mid-M splits)
 SPLITK_COUNTERS = 8192
 _SPLITK_WS: dict = {}
 
@@ -414,11 +434,11 @@ def _ksplit(proj: str, x: torch.Tensor, ksplit: int | None, tiles: int) -> int:
 
 def skinny_ok(x: torch.Tensor, w: torch.Tensor, preshuffled: bool = False,
               fp8: bool = False) -> bool:
-    """Does ``x @ w.T`` run on the MFMA weight-streaming kernels?  <= SKINNY_MAX_M rows on
-    any 16-bit / fp8 layout (gemv.hip); up to WIDE_MAX_M rows on pre-shuffled 16-bit weights
-    (wide.hip)."""
+    """Does ``x @ w.T`` run on the hand-written MFMA kernels?  <= SKINNY_MAX_M rows on any
+    16-bit / fp8 layout (gemv.hip); up to ``fused_max_rows()`` rows on pre-shuffled 16-bit
+    weights (wide.hip to 128 rows, midm.hip beyond)."""
     m, k = x.shape
-    lim = WIDE_MAX_M if (preshuffled and not fp8 and WIDE_MAX_M > SKINNY_MAX_M) else SKINNY_MAX_M
+    lim = fused_max_rows(preshuffled, fp8)
     return (x.is_cuda and 1 <= m <= lim and w.shape[0] % 16 == 0
             and k % 128 == 0 and x.stride(1) == 1 and w.is_contiguous())
 
@@ -429,23 +449,52 @@ def set_wide_plan(waves: int = 0, ksplit: int = 0) -> None:
     _native().set_wide_plan(int(waves), int(ksplit))
 
 
+def set_midm_plan(bmt: int = 0, ksplit: int = 0) -> None:
+    """Override the (row-block height 16 * bmt, K slices) plan of the NEXT mid-M launch
+    (tuning sweeps, warm-up); 0 = the kernel library's own plan."""
+    _native().set_midm_plan(int(bmt), int(ksplit))
+
+
+def midm_plan(m: int, ntiles: int, k: int, epi: int) -> tuple[int, int]:
+    """(bmt, K slices) the mid-M kernel plans for m rows x ntiles 16-column tiles x K (epi:
+    0 plain, 1 residual add, 2 qkv + RoPE, 3 gate_up + SiLU)."""
+    b, s = _native().midm_plan(int(m), int(ntiles), int(k), int(epi), SPLITK_WS_FLOATS)
+    return int(b), int(s)
+
+
+MIDM_BUILT = (3, 4, 5, 6, 8, 10, 12)  # row-block heights / 16 (csrc/midm_b<N>.hip)
+
+
 def warm_wide_kernels(device, dtype=torch.bfloat16) -> None:
-    """Launch one tiny wide GEMM per 16-row block count (1-8), so every per-block-count code
-    object (ops/csrc/wide_mt<N>.hip) is loaded at engine start: HIP loads a translation unit's
-    code object at the first launch of one of its kernels, which otherwise lands inside a
-    timed prefill (1.5-2.5 ms per object: burst TTFT 4.7 -> 6.3 / 7.3 ms the first time a
-    50 / 95-row burst ran, scripts/gpu/probe_fanout_ttft.py)."""
+    """Launch one tiny GEMM from every translation unit of the wide (wide_mt<N>.hip: one per
+    16-row block count the limits allow) and mid-M kernels (midm_b<N>.hip per row-block
+    height, midm.hip's split-K reduce), so every code object is loaded at engine start: HIP
+    loads a translation unit's code object at the first launch of one of its kernels, which
+    otherwise lands inside a timed prefill (1.5-2.5 ms per object: burst TTFT 4.7 -> 6.3 / 7.3
+    ms the first time a 50 / 95-row burst ran, scripts/gpu/probe_fanout_ttft.py).  Only
+    kernels the configured limits can route to are launched, and the caller's wide row
+    thresholds are restored afterwards."""
     dev = torch.device(device)
-    if dev.type != "cuda":
+    top = fused_max_rows(True, False)
+    if dev.type != "cuda" or top <= SKINNY_MAX_M:
         return
     ensure_splitk_workspace(dev)
     w = preshuffle(torch.zeros(128, 256, dtype=dtype, device=dev))
+    prev = [int(v) for v in _native().get_wide_min_rows()]
     set_wide_min_rows(1, 1)
     try:
         for mt in range(1, 9):
-            linear(torch.zeros(16 * mt, 256, dtype=dtype, device=dev), w, preshuffled=True)
+            if 16 * mt <= min(top, 128):
+                linear(torch.zeros(16 * mt, 256, dtype=dtype, device=dev), w, preshuffled=True)
+        if top > 128:
+            x = torch.zeros(144, 256, dtype=dtype, device=dev)
+            for b in MIDM_BUILT:
+                set_midm_plan(b, 1)
+                linear(x, w, preshuffled=True)
+            set_midm_plan(6, 2)  # the split-K reduce launch (midm.hip)
+            linear(x, w, preshuffled=True)
     finally:
-        set_wide_min_rows()
+        set_wide_min_rows(*prev)
     torch.cuda.synchronize(dev)
 
 

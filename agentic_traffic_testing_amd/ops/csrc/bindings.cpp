@@ -364,6 +364,21 @@ void set_wide_plan(int64_t waves, int64_t ksplit) {
   atta_set_wide_plan(static_cast<int>(waves), static_cast<int>(ksplit));
 }
 void set_flash_waves(int64_t nw) { atta_set_flash_waves(static_cast<int>(nw)); }
+std::vector<int64_t> get_wide_min_rows() {
+  int m = 0, ms = 0;
+  atta_get_wide_min_rows(&m, &ms);
+  return {m, ms};
+}
+void set_midm_plan(int64_t bmt, int64_t ksplit) {
+  atta_set_midm_plan(static_cast<int>(bmt), static_cast<int>(ksplit));
+}
+std::vector<int64_t> midm_plan(int64_t M, int64_t ntiles, int64_t K, int64_t epi,
+                               int64_t ws_floats) {
+  int bmt = 0, ks = 0;
+  atta_midm_plan(static_cast<int>(M), static_cast<int>(ntiles), static_cast<int>(K),
+                 static_cast<int>(epi), ws_floats, &bmt, &ks);
+  return {bmt, ks};
+}
 void set_wide_min_rows(int64_t m, int64_t m_silu) {
   atta_set_wide_min_rows(static_cast<int>(m), static_cast<int>(m_silu));
 }
@@ -824,6 +839,9 @@ TORCH_LIBRARY(atta, m) {
   m.def("prefill_gemm_error_reset() -> ()", &prefill_gemm_error_reset);
   m.def("set_wide_plan(int waves, int ksplit) -> ()", &set_wide_plan);
   m.def("set_wide_min_rows(int m, int m_silu) -> ()", &set_wide_min_rows);
+  m.def("get_wide_min_rows() -> int[]", &get_wide_min_rows);
+  m.def("set_midm_plan(int bmt, int ksplit) -> ()", &set_midm_plan);
+  m.def("midm_plan(int M, int ntiles, int K, int epi, int ws_floats) -> int[]", &midm_plan);
   m.def("set_flash_waves(int nw) -> ()", &set_flash_waves);
   m.def("prefill_gemm_config(int schedule, int group_m, int ablate=0) -> ()", &prefill_gemm_config);
   m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");

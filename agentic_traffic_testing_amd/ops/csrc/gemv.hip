@@ -213,6 +213,12 @@ void atta_set_wide_min_rows(int m, int m_silu) {
   g_wide_min_m = m < 1 ? 1 : m;
   g_wide_min_m_silu = m_silu < 1 ? 1 : m_silu;
 }
+void atta_get_wide_min_rows(int* m, int* m_silu) {
+  *m = g_wide_min_m;
+  *m_silu = g_wide_min_m_silu;
+}
+// pre-shuffled 16-bit calls of up to this many rows run the wide (<= 128) or mid-M kernels
+constexpr int kMidmMaxM = 8192;
 static bool use_wide(int M, int ps, const float* wscale, bool silu = false) {
   return M > 32 ||
          (ps && wscale == nullptr && M >= (silu ? g_wide_min_m_silu : g_wide_min_m));
@@ -240,10 +246,17 @@ int atta_set_splitk_ws(int device, float* ws, int* counters, int64_t ws_floats, 
   return 0;
 }
 
+int atta_midm_launch(SkinnyParams& p, int epi, int ntiles, int dtype, float* sk_ws,
+                     int64_t ws_floats, hipStream_t stream);
 static int wide(SkinnyParams& p, int epi, int ntiles, int dtype, hipStream_t stream) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -2;
   const SplitKWs& w = g_splitk[dev];
+  if (p.M > 128) {
+    // past the wide kernel's 8 row blocks: the mid-M kernel (midm.hip, row-blocked grid)
+    p.wg_trace = nullptr;
+    return atta_midm_launch(p, epi, ntiles, dtype, w.ws, w.ws_floats, stream);
+  }
   const int waves = g_wide_waves, ksplit = g_wide_ksplit;
   g_wide_waves = g_wide_ksplit = 0;
   p.wg_trace = take_trace();  // 4 stamps per workgroup here (wide.hip)
@@ -279,7 +292,7 @@ int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual
                      int ksplit, const float* wscale, int dtype, hipStream_t stream) {
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
-  if (M < 1 || M > (ps && wscale == nullptr ? 128 : 32) || N % 16 != 0) return -1;
+  if (M < 1 || M > (ps && wscale == nullptr ? kMidmMaxM : 32) || N % 16 != 0) return -1;
   SkinnyParams p{};
   p.ps = ps;
   p.wscale = wscale;
@@ -357,7 +370,7 @@ int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x
                         int dtype, hipStream_t stream) {
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
-  if (M < 1 || M > (ps && wscale == nullptr ? 128 : 32)) return -1;
+  if (M < 1 || M > (ps && wscale == nullptr ? kMidmMaxM : 32)) return -1;
   int shift = 0;
   while ((1 << shift) < block_size) ++shift;
   if ((1 << shift) != block_size) return -1;
@@ -394,7 +407,7 @@ int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int 
                             int ksplit, const float* wscale, int dtype, hipStream_t stream) {
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
-  if (M < 1 || M > (ps && wscale == nullptr ? 128 : 32) || inter % 8 != 0) return -1;
+  if (M < 1 || M > (ps && wscale == nullptr ? kMidmMaxM : 32) || inter % 8 != 0) return -1;
   SkinnyParams p{};
   p.ps = ps;
   p.wscale = wscale;

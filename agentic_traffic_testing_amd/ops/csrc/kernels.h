@@ -151,5 +151,10 @@ int atta_prefill_gemm_error_async(void* host, hipStream_t stream, int clear);
 int atta_prefill_gemm_error_reset();
 void atta_set_wide_plan(int waves, int ksplit);
 void atta_set_wide_min_rows(int m, int m_silu);
+void atta_get_wide_min_rows(int* m, int* m_silu);
+// mid-M GEMM (midm.hip): the next launch's plan (row-block height bmt x 16, K slices; 0 =
+// planned) and the plan the library would pick for a shape
+void atta_set_midm_plan(int bmt, int ksplit);
+int atta_midm_plan(int M, int ntiles, int K, int epi, int64_t ws_floats, int* bmt, int* ksplit);
 void atta_set_flash_waves(int nw);
 int atta_prefill_gemm_config(int schedule, int group_m, int ablate);

@@ -72,6 +72,8 @@ def main():
                     help="M <= 32: wide kernel vs the 16-row-tile GEMV (second column)")
     ap.add_argument("--sweep", action="store_true",
                     help="every (waves, split) plan; prints the best per (proj, M)")
+    ap.add_argument("--midm-sweep", action="store_true",
+                    help="M > 128: every (row-block height, K split) plan of the mid-M kernel")
     a = ap.parse_args()
     global GRAPH
     GRAPH = a.graph
@@ -99,8 +101,9 @@ def main():
             q = torch.empty(m, hq, 128, dtype=dt, device="cuda")
             act = torch.empty(m, n // 2, dtype=dt, device="cuda")
 
-            def wide(i, plan=(0, 0)):
+            def wide(i, plan=(0, 0), mplan=(0, 0)):
                 ops.set_wide_plan(*plan)
+                ops.set_midm_plan(*mplan)
                 w = wps[i % ncopy]
                 if proj == "qkv":
                     ops.decode_qkv_rope(x, w, 1e-5, pos, slots, cs, kc, vc, hq, hkv, q_out=q,
@@ -134,6 +137,22 @@ def main():
             tot[m][1] += tl
             line = (f"{proj:8s} M={m:4d} | wide {tw:7.1f} us ({mb / tw:5.2f} TB/s) | "
                     f"library {tl:7.1f} us | {tl / tw:5.2f}x")
+            if m > 128:
+                epi = {"qkv": 2, "gate_up": 3, "o": 1, "down": 1}[proj]
+                ntiles = n // 8 // 2 if proj == "gate_up" else n // 16
+                line += " | plan bmt %d S %d" % ops.midm_plan(m, ntiles, k, epi)
+            if a.midm_sweep and m > 128:
+                tim = {}
+                splits = (1,) if proj in ("qkv", "gate_up") else (1, 2, 3, 4, 6, 8)
+                for b_ in ops.MIDM_BUILT:
+                    for s_ in splits:
+                        try:
+                            tim[(b_, s_)] = timeit(lambda i, p=(b_, s_): wide(i, mplan=p), n=20)
+                        except RuntimeError:
+                            pass
+                best = min(tim, key=tim.get)
+                line += (f" | best {best[0]}x{best[1]}={tim[best]:.1f} | " +
+                         " ".join(f"{k[0]}x{k[1]}={v:.1f}" for k, v in sorted(tim.items())))
             if a.sweep:
                 tim = {}
                 for w_ in (4, 6, 7, 8):

@@ -484,16 +484,18 @@ def test_fp8_engine_matches_fp32_oracle(model, prefill_gemm):
     # (activations moved across e4m3 rounding boundaries by the oracle's fp32 attention), but
     # a drifting fp8 path would flip most positions of most sequences: both bounds sit below
     # that.  Small model: at most 2 divergent sequences, 1 position in 5.  70B slice (flat
-    # random-init logits, where a re-ordered fp32 sum in decode attention already moves a
-    # few prefill activations across e4m3 boundaries): at most 1 position in 3 - every flip
-    # still a < 0.3-logit near tie against the oracle on the engine's own prefix
+    # random-init logits): the same 1 position in 5, but no sequence bound - the 8-wave decode
+    # attention default (round 5) re-orders its fp32 sums, which moves a few activations
+    # across e4m3 boundaries in every sequence (5 of 5 diverged once, 8 of 40 positions at
+    # worst: profiles/r5_gpu_tier_final2.log); every flip is still a < 0.3-logit near tie
+    # against the oracle on the engine's own prefix
     print("fp8 oracle", model, prefill_gemm, "bad_seqs", bad_seqs, "bad_pos", bad_pos, "of", checked)
     assert checked == 8 * len(prompts)
     if model == "small":
         assert bad_seqs <= 2, (bad_seqs, bad_pos)
         assert bad_pos <= checked // 5, (bad_seqs, bad_pos)
     else:
-        assert bad_pos <= checked // 3, (bad_seqs, bad_pos)
+        assert bad_pos <= checked // 5, (bad_seqs, bad_pos)
     assert eng.runner.graph_steps > 0
 
 
@@ -629,3 +631,54 @@ def test_small_prefill_fused_matches_unfused_and_oracle():
     for a, b in zip(caches[True], caches[False]):
         tol = 0.03 * float(b.abs().max()) + 1e-3
         assert float((a - b).abs().max()) <= tol, float((a - b).abs().max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", ["small", "llama-8b-slice"])
+def test_midm_prefill_engine_matches_oracle(model):
+    """Uncached prefill steps of 129-1024 rows run the fused mid-M kernels (ops/csrc/midm.h:
+    RMSNorm-folded qkv + RoPE + paged K/V write, o / down residual add with split-K, gate_up
+    + SiLU-mul) inside the engine; teacher-forced greedy tokens against the fp32 dense oracle
+    (near-tie rule), a 400-row first step and a 700-row one."""
+    vocab = 30000 if model == "small" else 16000
+    cfg = EngineConfig(model=model, device="cuda", max_model_len=1024, num_kv_blocks=1024,
+                       max_num_batched_tokens=2048, max_num_seqs=8,
+                       graph_batch_sizes=(1, 2, 4, 8))
+    eng = LLMEngine(cfg)
+    m = eng.runner.model
+    assert m.small_prefill_ok(400) and m.small_prefill_ok(700)
+    rng = np.random.default_rng(11)
+    for sizes in ((150, 95, 80, 60, 15), (700,)):
+        prompts = [rng.integers(300, vocab, size=n).tolist() for n in sizes]
+        outs, bad = _check(eng, prompts, n=5, tol_logit=0.25)
+        assert bad <= max(1, len(prompts) // 2)
+
+
+@pytest.mark.gpu
+def test_engine_starts_with_wide_kernel_off():
+    """ATTA_WIDE_MAX_M=0 turns the wide / mid-M kernels off - the engine must start
+    (no warm-up launch of a kernel the limits exclude) and serve a 48-row prefill on the
+    library path; the native <= 32-row routing stays off the wide kernel too."""
+    import os
+    import subprocess
+    import sys
+
+    code = (
+        "from agentic_traffic_testing_amd.config import EngineConfig\n"
+        "from agentic_traffic_testing_amd.engine.llm_engine import LLMEngine\n"
+        "from agentic_traffic_testing_amd.engine.sequence import SamplingParams\n"
+        "from agentic_traffic_testing_amd import ops\n"
+        "assert ops.fused_max_rows() == ops.SKINNY_MAX_M\n"
+        "eng = LLMEngine(EngineConfig(model='small', device='cuda', max_model_len=512,\n"
+        "                             num_kv_blocks=256, max_num_seqs=4,\n"
+        "                             graph_batch_sizes=(1, 2, 4)))\n"
+        "assert not eng.runner.model.small_prefill_ok(48)\n"
+        "assert list(ops._native().get_wide_min_rows()) == [33, 33]\n"
+        "outs = eng.generate([list(range(300, 348)), list(range(400, 420))],\n"
+        "                    SamplingParams(temperature=0.0, max_tokens=4, ignore_eos=True))\n"
+        "assert all(len(o.token_ids) == 4 for o in outs)\n"
+        "print('ok')\n")
+    env = dict(os.environ, ATTA_WIDE_MAX_M="0", ATTA_NO_BUILD="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
