@@ -334,24 +334,28 @@ class LlamaModel:
         # row-major skinny / library GEMMs (17 rows: 168 -> ~80 us of GEMMs per layer,
         # profiles/r4_small_prefill_fused.txt)
         small = self.small_prefill_ok(T)
+        # 129..640-row steps (uncached burst / planning prefills): per projection, the mid-M
+        # kernel (ops/csrc/midm.h, fused epilogues) where it beats the tuned library GEMM +
+        # separate norm / RoPE / SiLU kernels, the library elsewhere (midm_route)
+        mid = {} if (small or fp8) else self.midm_route(T)
         for li, L in enumerate(self.layers):
             ps = L.qkv_ps is not None
-            if small:
+            if small or mid.get("qkv"):
                 q = ops.decode_qkv_rope(residual, L.qkv_ps if ps else L.qkv, eps, md.positions,
                                         md.slot_mapping, self.cos_sin, k_caches[li],
                                         v_caches[li], nq, nkv, preshuffled=ps)
-            elif fp8:
-                if pending is None:
-                    xq, xs = ops.quant_rows_fp8(residual, ops.QUANT_NORM, L.input_norm, eps)
-                else:
-                    xq, xs = ops.quant_rows_fp8(pending, ops.QUANT_ADDNORM, L.input_norm, eps,
-                                                residual)
-                qkv = self._gemm8(xq, xs, L.qkv, L.qkv_s, dt, "qkv")
-            elif self._pg(T, L.qkv, proj="qkv"):
-                qkv = ops.prefill_gemm(ops.rms_norm(residual, L.input_norm, eps), L.qkv)
             else:
-                qkv = self._proj(ops.rms_norm(residual, L.input_norm, eps), L.qkv, L.qkv_s)
-            if not small:
+                if fp8:
+                    if pending is None:
+                        xq, xs = ops.quant_rows_fp8(residual, ops.QUANT_NORM, L.input_norm, eps)
+                    else:
+                        xq, xs = ops.quant_rows_fp8(pending, ops.QUANT_ADDNORM, L.input_norm,
+                                                    eps, residual)
+                    qkv = self._gemm8(xq, xs, L.qkv, L.qkv_s, dt, "qkv")
+                elif self._pg(T, L.qkv, proj="qkv"):
+                    qkv = ops.prefill_gemm(ops.rms_norm(residual, L.input_norm, eps), L.qkv)
+                else:
+                    qkv = self._proj(ops.rms_norm(residual, L.input_norm, eps), L.qkv, L.qkv_s)
                 q = ops.rope_cache(qkv, md.positions, md.slot_mapping, self.cos_sin,
                                    k_caches[li], v_caches[li], nq, nkv, D)
             attn = torch.empty_like(q)
@@ -376,24 +380,28 @@ class LlamaModel:
                     aq, as_ = ops.quant_rows_fp8(gu, ops.QUANT_SILU)
                 pending = self._all_reduce(self._gemm8(aq, as_, L.down, L.down_s, dt, "down"))
                 continue
-            if small:
+            if small or mid.get("o"):
                 ops.linear(attn.view(T, nq * D), L.o_ps if ps else L.o, residual=residual,
                            waves=ops.decode_waves("o", ps, False), preshuffled=ps, ksplit=None,
                            proj="o")
+            else:
+                self._proj_residual(attn.view(T, nq * D), L.o, L.o_s, residual, "o")
+            if small or mid.get("gate_up"):
                 a = ops.decode_gate_up_silu(residual, L.gate_up_ps if ps else L.gate_up, eps,
                                             preshuffled=ps)
+            else:
+                x = ops.rms_norm(residual, L.post_norm, eps)
+                if self._pg(T, L.gate_up, mode=ops.GEMM_SILU, proj="gate_up"):
+                    a = ops.prefill_gemm(x, L.gate_up, ops.GEMM_SILU)
+                else:
+                    gu = self._proj(x, L.gate_up, L.gate_up_s)
+                    a = ops.silu_and_mul(gu)
+            if small or mid.get("down"):
                 ops.linear(a, L.down_ps if ps else L.down, residual=residual,
                            waves=ops.decode_waves("down", ps, False), preshuffled=ps,
                            ksplit=None, proj="down")
-                continue
-            self._proj_residual(attn.view(T, nq * D), L.o, L.o_s, residual, "o")
-            x = ops.rms_norm(residual, L.post_norm, eps)
-            if self._pg(T, L.gate_up, mode=ops.GEMM_SILU, proj="gate_up"):
-                a = ops.prefill_gemm(x, L.gate_up, ops.GEMM_SILU)
             else:
-                gu = self._proj(x, L.gate_up, L.gate_up_s)
-                a = ops.silu_and_mul(gu)
-            self._proj_residual(a, L.down, L.down_s, residual, "down")
+                self._proj_residual(a, L.down, L.down_s, residual, "down")
         if rows is not None:
             residual = residual.index_select(0, rows)
             pending = None if pending is None else pending.index_select(0, rows)
@@ -473,14 +481,37 @@ class LlamaModel:
             return self.tp_group.all_reduce_residual(self._proj(x, w, scale), residual)
         return self._proj(x, w, scale, residual=residual)
 
+    # Per-projection row ranges where the mid-M kernel (fused epilogues included) beat the tuned
+    # library GEMM plus its separate norm / RoPE / SiLU kernels at the 8B shapes, cold weights,
+    # library rows padded to the tuning buckets as the engine runs them
+    # (profiles/r6_midm_vs_tuned.txt): qkv + RoPE 1.05-1.48x at 129-640 rows, down + residual
+    # 1.03-1.41x at 129-640, o + residual 1.05-1.17x at 129-188 and 1.06-1.12x at 448-640;
+    # gate_up + SiLU loses everywhere (0.59-0.93x: the kernel streams ~52 GB/s per CU at ~35 %
+    # MFMA, the library's 256-wide tiles run ~41 %).
+    MIDM_ROUTES = {"qkv": ((129, 640),), "o": ((129, 188), (448, 640)), "gate_up": (),
+                   "down": ((129, 640),)}
+
+    def midm_route(self, T: int) -> dict:
+        """{projection: True} for the projections of a T-row step that run the mid-M kernel
+        (empty when the step cannot: TP, fp8, no pre-shuffled weights, rows past
+        ops.MIDM_MAX_M)."""
+        if (T <= 128 or T > ops.fused_max_rows(True, False) or self.quant == "fp8"
+                or self.tp_size != 1 or not self.fused_decode or not self.small_prefill_fused
+                or not self.decode_fusable(min(T, 128)) or not self.layers
+                or self.layers[0].qkv_ps is None):
+            return {}
+        return {p: any(lo <= T <= hi for lo, hi in r) for p, r in self.MIDM_ROUTES.items()}
+
     def small_prefill_ok(self, T: int) -> bool:
         """Does a (prefill or mixed) step of T rows run on the fused decode kernels - RMSNorm
         folded into the pre-shuffled skinny GEMVs, RoPE + KV write in the QKV epilogue, SiLU-mul
         in gate_up?  The one predicate for forward() and the runner's row padding (ADVICE r4:
         TP / fp8 steps of <= 32 rows take the library path and must be padded to its tuned
-        buckets; fused_decode=False turns the fused kernels off here too)."""
+        buckets; fused_decode=False turns the fused kernels off here too).  Up to 128 rows:
+        past that every projection is routed on its own (midm_route)."""
         return (self.small_prefill_fused and self.fused_decode and self.device.type == "cuda"
-                and self.tp_size == 1 and self.quant != "fp8" and self.decode_fusable(T))
+                and self.tp_size == 1 and self.quant != "fp8" and T <= 128
+                and self.decode_fusable(T))
 
     def decode_fusable(self, num_tokens: int) -> bool:
         """Can a step of this many rows run the fused weight-streaming kernels?  <= 32 rows:

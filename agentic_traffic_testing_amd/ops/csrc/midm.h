@@ -53,7 +53,7 @@ struct Geo {
   int R;            // rows of the split-K slab layout (M padded to 16)
 };
 
-template <typename T, int BMT, int EPI, bool NORM>
+template <typename T, int BMT, int EPI, bool NORM, int XD>
 __global__ __launch_bounds__(kThr) void midm_kernel(SkinnyParams p, Geo g) {
   using MF = MfmaK32<T>;
   using frag8 = typename MF::frag8;
@@ -62,10 +62,15 @@ __global__ __launch_bounds__(kThr) void midm_kernel(SkinnyParams p, Geo g) {
   constexpr int PPT = (PIECES + kThr - 1) / kThr;  // x pieces per thread per chunk
   constexpr int XBUF = BM * kRowB;
   constexpr int REDB = kTPB * BM * 17 * 4;
-  constexpr int LDSB = 2 * XBUF > REDB ? 2 * XBUF : REDB;
+  // XD (deep x pipeline, built for <= 128-row blocks): three x register sets loaded three
+  // chunks ahead into three LDS buffers, three weight stages - the LDS write of a chunk waits
+  // for loads issued two chunks earlier (qkv at 382 rows 38.7 -> 36.1 us); larger blocks keep
+  // two x sets / buffers (three buffers of 192 rows cost them their LDS headroom)
+  constexpr int NXB = XD == 1 ? 3 : 2;
+  constexpr int LDSB = NXB * XBUF > REDB ? NXB * XBUF : REDB;
   constexpr int NWF = kNTW * 2;  // weight fragments per chunk per wave (2 K steps x tiles)
   constexpr int RPL = (BM + 63) / 64;
-  constexpr int kWStages = wstages(BMT);
+  constexpr int kWStages = XD == 1 ? 3 : wstages(BMT);
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDSB];
   __shared__ float ssq[BM];
   __shared__ float inv_rms[BM];
@@ -119,7 +124,7 @@ __global__ __launch_bounds__(kThr) void midm_kernel(SkinnyParams p, Geo g) {
 #pragma unroll
   for (int i = 0; i < PPT; ++i) ss[i] = 0.f;
 
-  u32x4 w0[NWF], w1[NWF], w2[NWF], w3[NWF], xa[PPT], xb[PPT];
+  u32x4 w0[NWF], w1[NWF], w2[NWF], w3[NWF], xa[PPT], xb[PPT], xc[PPT];
   auto load_w = [&](u32x4 (&f)[NWF], int c) {
 #pragma unroll
     for (int j = 0; j < kNTW; ++j)
@@ -146,18 +151,43 @@ __global__ __launch_bounds__(kThr) void midm_kernel(SkinnyParams p, Geo g) {
       }
     }
   };
-  // this wave's two K steps of the chunk in `buf`: each x fragment feeds both tiles' MFMAs
+  // this wave's two K steps of the chunk in `buf`: each x fragment feeds both tiles' MFMAs.
+  // Every fragment read of the chunk is issued before the first MFMA (up to 8 row blocks:
+  // the register budget): waiting on each ds_read right before its two MFMAs left the
+  // waves idle on LDS latency between MFMA pairs (one barrier per chunk, two waves per SIMD)
   auto compute = [&](const u32x4 (&f)[NWF], int buf) {
     const unsigned char* bb = lds + buf * XBUF + col * kRowB;
+    if constexpr (BMT <= 8) {
+      frag8 xf[2][BMT];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int off = (((2 * kg + s) * 4 + grp) ^ col) << 4;
+      for (int s = 0; s < 2; ++s) {
+        const int off = (((2 * kg + s) * 4 + grp) ^ col) << 4;
 #pragma unroll
-      for (int t = 0; t < BMT; ++t) {
-        const frag8 xf = *reinterpret_cast<const frag8*>(bb + t * 16 * kRowB + off);
+        for (int t = 0; t < BMT; ++t)
+          xf[s][t] = *reinterpret_cast<const frag8*>(bb + t * 16 * kRowB + off);
+      }
 #pragma unroll
-        for (int j = 0; j < kNTW; ++j)
-          acc[j][t] = MF::mma(xf, __builtin_bit_cast(frag8, f[j * 2 + s]), acc[j][t]);
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < BMT; ++t)
+#pragma unroll
+          for (int j = 0; j < kNTW; ++j)
+            acc[j][t] = MF::mma(xf[s][t], __builtin_bit_cast(frag8, f[j * 2 + s]), acc[j][t]);
+      // pin the order (hipcc otherwise sinks each read next to its MFMA pair): all reads,
+      // then the MFMAs, with counted lgkmcnt waits between them
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * BMT, 0);          // DS read
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * BMT * kNTW, 0);   // MFMA
+    } else {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int off = (((2 * kg + s) * 4 + grp) ^ col) << 4;
+#pragma unroll
+        for (int t = 0; t < BMT; ++t) {
+          const frag8 xf = *reinterpret_cast<const frag8*>(bb + t * 16 * kRowB + off);
+#pragma unroll
+          for (int j = 0; j < kNTW; ++j)
+            acc[j][t] = MF::mma(xf, __builtin_bit_cast(frag8, f[j * 2 + s]), acc[j][t]);
+        }
       }
     }
   };
@@ -166,7 +196,14 @@ __global__ __launch_bounds__(kThr) void midm_kernel(SkinnyParams p, Geo g) {
                   u32x4 (&xload)[PPT], int c, int buf) {
     load_x(xload, min(c + 2, clast));
     load_w(wnext, min(c + kWStages - 1, clast));
+    // keep the prefetches at the top of the chunk: left alone, hipcc sinks them below the
+    // MFMAs and the stores, so the x loads led their LDS write by under a chunk and the
+    // kernel ran latency-bound (48 GB/s per CU at 382 rows)
+    __builtin_amdgcn_sched_barrier(0);
     compute(wcur, buf);
+    // and the LDS writes of the next chunk after the MFMAs (their wait on the x loads must
+    // not stall the chunk's MFMAs)
+    __builtin_amdgcn_sched_barrier(0);
     store_x(xstage, buf ^ 1, c + 1 < c1);
     // LDS hand-over only (wide.h: a bare s_barrier keeps the register loads in flight)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -174,50 +211,85 @@ __global__ __launch_bounds__(kThr) void midm_kernel(SkinnyParams p, Geo g) {
     asm volatile("" ::: "memory");
   };
 
-  if (c0 < c1) {
-    load_x(xa, c0);
-    load_w(w0, c0);
-    load_x(xb, min(c0 + 1, clast));
-    load_w(w1, min(c0 + 1, clast));
-    if constexpr (kWStages == 4) load_w(w2, min(c0 + 2, clast));
-    store_x(xa, 0, true);
-  }
-  __syncthreads();
-  int c = c0;
-  if constexpr (kWStages == 4) {
-    // whole 4-chunk periods (4 weight stages x 2 x sets), then the <= 3 remaining chunks
-    for (; c + 4 <= c1; c += 4) {
-      iter(w0, w3, xb, xa, c, 0);
-      iter(w1, w0, xa, xb, c + 1, 1);
-      iter(w2, w1, xb, xa, c + 2, 0);
-      iter(w3, w2, xa, xb, c + 3, 1);
+  if constexpr (XD == 1) {
+    // chunk c (r = c - c0): weights in stage r % 3, x in register set r % 3, LDS buffer r % 3
+    auto iter3 = [&](const u32x4 (&wcur)[NWF], u32x4 (&wnext)[NWF], const u32x4 (&xw)[PPT],
+                     u32x4 (&xl)[PPT], int c, int buf) {
+      load_x(xl, min(c + 3, clast));
+      load_w(wnext, min(c + 2, clast));
+      __builtin_amdgcn_sched_barrier(0);
+      compute(wcur, buf);
+      __builtin_amdgcn_sched_barrier(0);
+      store_x(xw, buf == 2 ? 0 : buf + 1, c + 1 < c1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    if (c0 < c1) {
+      load_x(xa, c0);
+      load_w(w0, c0);
+      load_x(xb, min(c0 + 1, clast));
+      load_w(w1, min(c0 + 1, clast));
+      load_x(xc, min(c0 + 2, clast));
+      store_x(xa, 0, true);
+    }
+    __syncthreads();
+    int c = c0;
+    for (; c + 3 <= c1; c += 3) {
+      iter3(w0, w2, xb, xa, c, 0);
+      iter3(w1, w0, xc, xb, c + 1, 1);
+      iter3(w2, w1, xa, xc, c + 2, 2);
     }
     if (c < c1) {
-      iter(w0, w3, xb, xa, c, 0);
-      if (c + 1 < c1) {
-        iter(w1, w0, xa, xb, c + 1, 1);
-        if (c + 2 < c1) iter(w2, w1, xb, xa, c + 2, 0);
-      }
+      iter3(w0, w2, xb, xa, c, 0);
+      if (c + 1 < c1) iter3(w1, w0, xc, xb, c + 1, 1);
     }
   } else {
-    // whole 6-chunk periods (3 weight stages x 2 x sets), then the <= 5 remaining chunks
-    for (; c + 6 <= c1; c += 6) {
-      iter(w0, w2, xb, xa, c, 0);
-      iter(w1, w0, xa, xb, c + 1, 1);
-      iter(w2, w1, xb, xa, c + 2, 0);
-      iter(w0, w2, xa, xb, c + 3, 1);
-      iter(w1, w0, xb, xa, c + 4, 0);
-      iter(w2, w1, xa, xb, c + 5, 1);
+    if (c0 < c1) {
+      load_x(xa, c0);
+      load_w(w0, c0);
+      load_x(xb, min(c0 + 1, clast));
+      load_w(w1, min(c0 + 1, clast));
+      if constexpr (kWStages == 4) load_w(w2, min(c0 + 2, clast));
+      store_x(xa, 0, true);
     }
-    if (c < c1) {
-      iter(w0, w2, xb, xa, c, 0);
-      if (c + 1 < c1) {
+    __syncthreads();
+    int c = c0;
+    if constexpr (kWStages == 4) {
+      // whole 4-chunk periods (4 weight stages x 2 x sets), then the <= 3 remaining chunks
+      for (; c + 4 <= c1; c += 4) {
+        iter(w0, w3, xb, xa, c, 0);
         iter(w1, w0, xa, xb, c + 1, 1);
-        if (c + 2 < c1) {
-          iter(w2, w1, xb, xa, c + 2, 0);
-          if (c + 3 < c1) {
-            iter(w0, w2, xa, xb, c + 3, 1);
-            if (c + 4 < c1) iter(w1, w0, xb, xa, c + 4, 0);
+        iter(w2, w1, xb, xa, c + 2, 0);
+        iter(w3, w2, xa, xb, c + 3, 1);
+      }
+      if (c < c1) {
+        iter(w0, w3, xb, xa, c, 0);
+        if (c + 1 < c1) {
+          iter(w1, w0, xa, xb, c + 1, 1);
+          if (c + 2 < c1) iter(w2, w1, xb, xa, c + 2, 0);
+        }
+      }
+    } else {
+      // whole 6-chunk periods (3 weight stages x 2 x sets), then the <= 5 remaining chunks
+      for (; c + 6 <= c1; c += 6) {
+        iter(w0, w2, xb, xa, c, 0);
+        iter(w1, w0, xa, xb, c + 1, 1);
+        iter(w2, w1, xb, xa, c + 2, 0);
+        iter(w0, w2, xa, xb, c + 3, 1);
+        iter(w1, w0, xb, xa, c + 4, 0);
+        iter(w2, w1, xa, xb, c + 5, 1);
+      }
+      if (c < c1) {
+        iter(w0, w2, xb, xa, c, 0);
+        if (c + 1 < c1) {
+          iter(w1, w0, xa, xb, c + 1, 1);
+          if (c + 2 < c1) {
+            iter(w2, w1, xb, xa, c + 2, 0);
+            if (c + 3 < c1) {
+              iter(w0, w2, xa, xb, c + 3, 1);
+              if (c + 4 < c1) iter(w1, w0, xb, xa, c + 4, 0);
+            }
           }
         }
       }
@@ -298,7 +370,7 @@ __global__ __launch_bounds__(kThr) void midm_kernel(SkinnyParams p, Geo g) {
 constexpr bool norm_fits(int bmt) { return bmt <= 8; }
 
 // launch one (BMT) instantiation; -1 = epilogue / norm combination not built
-template <typename T, int BMT>
+template <typename T, int BMT, int XD>
 inline int launch_bmt(int epi, dim3 grid, hipStream_t st, const SkinnyParams& p, const Geo& g) {
   const dim3 blk(kThr);
   const bool norm = p.eps > 0.f;
@@ -308,19 +380,19 @@ inline int launch_bmt(int epi, dim3 grid, hipStream_t st, const SkinnyParams& p,
   switch (epi) {
     case EPI_PLAIN:
       if (norm) return -1;
-      midm_kernel<T, BMT, EPI_PLAIN, false><<<grid, blk, 0, st>>>(p, g);
+      midm_kernel<T, BMT, EPI_PLAIN, false, XD><<<grid, blk, 0, st>>>(p, g);
       return 0;
     case EPI_RESADD:
       if (norm) return -1;
-      midm_kernel<T, BMT, EPI_RESADD, false><<<grid, blk, 0, st>>>(p, g);
+      midm_kernel<T, BMT, EPI_RESADD, false, XD><<<grid, blk, 0, st>>>(p, g);
       return 0;
     case EPI_QKVROPE:
       if (!norm || g.S > 1) return -1;
-      if constexpr (norm_fits(BMT)) midm_kernel<T, BMT, EPI_QKVROPE, true><<<grid, blk, 0, st>>>(p, g);
+      if constexpr (norm_fits(BMT)) midm_kernel<T, BMT, EPI_QKVROPE, true, XD><<<grid, blk, 0, st>>>(p, g);
       return 0;
     case EPI_SILU:
       if (!norm || g.S > 1) return -1;
-      if constexpr (norm_fits(BMT)) midm_kernel<T, BMT, EPI_SILU, true><<<grid, blk, 0, st>>>(p, g);
+      if constexpr (norm_fits(BMT)) midm_kernel<T, BMT, EPI_SILU, true, XD><<<grid, blk, 0, st>>>(p, g);
       return 0;
     default: return -1;
   }
@@ -330,8 +402,9 @@ inline int launch_bmt(int epi, dim3 grid, hipStream_t st, const SkinnyParams& p,
 #define ATTA_MIDM_TU(N)                                                                       \
   int launch_b_##N(int epi, dim3 grid, hipStream_t st, const SkinnyParams& p, const Geo& g,   \
                    int dtype) {                                                               \
-    return dtype == 0 ? launch_bmt<__bf16, N>(epi, grid, st, p, g)                            \
-                      : launch_bmt<_Float16, N>(epi, grid, st, p, g);                         \
+    constexpr int xd = N <= 8 ? 1 : 0;                                                        \
+    return dtype == 0 ? launch_bmt<__bf16, N, xd>(epi, grid, st, p, g)                        \
+                      : launch_bmt<_Float16, N, xd>(epi, grid, st, p, g);                     \
   }
 
 }  // namespace midm

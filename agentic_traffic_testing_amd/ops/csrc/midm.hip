@@ -81,10 +81,13 @@ static int launch_tu(int bmt, int epi, dim3 grid, hipStream_t st, const SkinnyPa
 }
 
 // Cost model of one plan (us): rounds of the grid over the 256 CUs x a workgroup's time - the
-// larger of its MFMA time (75 % of the 16x16x32 issue rate) and its operand bytes at a per-CU
-// load rate - plus ramp; a split adds the reduce launch reading every slice's slab.
+// larger of its MFMA time and its operand bytes at a per-CU load rate - plus ramp; a split
+// adds the slab stores and the reduce launch.  Constants fitted to the round-6 sweep of every
+// (row block, split) plan at the 8B shapes, 188-475 rows (profiles/r6_midm_sweep.txt): a
+// workgroup streams ~52 GB/s and keeps the MFMA pipe ~35 % busy; split-K costs ~6 us plus
+// its slab traffic.
 struct Cost {
-  double mfma_eff = 0.75, cu_bps = 100e3, ramp = 1.5, red_fixed = 1.5, red_bps = 5e6;
+  double mfma_eff = 0.35, cu_bps = 52e3, ramp = 2.0, red_fixed = 6.0, red_bps = 1.5e6;
 };
 
 static double plan_cost(const Cost& c, int M, int ntiles, int K, int bmt, int S) {
@@ -138,6 +141,7 @@ void atta_set_midm_plan(int bmt, int ksplit) {
   g_midm_bmt = bmt;
   g_midm_ksplit = ksplit;
 }
+
 
 int atta_midm_plan(int M, int ntiles, int K, int epi, int64_t ws_floats, int* bmt, int* ksplit) {
   const bool can_split = epi == EPI_PLAIN || epi == EPI_RESADD;

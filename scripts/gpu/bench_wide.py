@@ -74,11 +74,17 @@ def main():
                     help="every (waves, split) plan; prints the best per (proj, M)")
     ap.add_argument("--midm-sweep", action="store_true",
                     help="M > 128: every (row-block height, K split) plan of the mid-M kernel")
+    ap.add_argument("--tuned", action="store_true",
+                    help="library arm on the shipped tuned table, rows padded to its buckets "
+                         "(as the engine runs it)")
     a = ap.parse_args()
     global GRAPH
     GRAPH = a.graph
     assert ops.native_available(), ops._load_error
     ops.ensure_splitk_workspace("cuda")
+    if a.tuned:
+        from agentic_traffic_testing_amd import tuning
+        print("tuned table:", tuning.load("auto", "llama-3.1-8b"), flush=True)
     dt = torch.bfloat16
     hq, hkv, bs, nb = 32, 8, 16, 512
     kc = torch.zeros(nb, hkv, bs, 128, dtype=dt, device="cuda")
@@ -114,15 +120,23 @@ def main():
                     ops.linear(x, w, residual=res, preshuffled=True, ksplit=None, proj=proj,
                                waves=ops.decode_waves(proj, True, False))
 
+            ml = m
+            if a.tuned and m > 32:
+                from agentic_traffic_testing_amd.tuning import bucket_rows
+                ml = bucket_rows(m)
+            xl = torch.randn(ml, k, device="cuda").to(dt)
+            resl = torch.zeros(ml, n, dtype=dt, device="cuda")
+            posl = torch.arange(ml, dtype=torch.int32, device="cuda")
+
             def lib(i):
                 w = raw[i % ncopy]
                 if proj == "qkv":
-                    y = torch.nn.functional.linear(ops.rms_norm(x, ones, 1e-5), w)
-                    ops.rope_cache(y, pos, slots, cs, kc, vc, hq, hkv, 128)
+                    y = torch.nn.functional.linear(ops.rms_norm(xl, ones, 1e-5), w)
+                    ops.rope_cache(y, posl, posl, cs, kc, vc, hq, hkv, 128)
                 elif proj == "gate_up":
-                    ops.silu_and_mul(torch.nn.functional.linear(ops.rms_norm(x, ones, 1e-5), w))
+                    ops.silu_and_mul(torch.nn.functional.linear(ops.rms_norm(xl, ones, 1e-5), w))
                 else:
-                    res.addmm_(x, w.t())
+                    resl.addmm_(xl, w.t())
 
             ops.set_wide_min_rows(*((1, 1) if a.wide_below_33 else (17, 12)))
             tw = timeit(wide)
@@ -142,17 +156,19 @@ def main():
                 ntiles = n // 8 // 2 if proj == "gate_up" else n // 16
                 line += " | plan bmt %d S %d" % ops.midm_plan(m, ntiles, k, epi)
             if a.midm_sweep and m > 128:
-                tim = {}
-                splits = (1,) if proj in ("qkv", "gate_up") else (1, 2, 3, 4, 6, 8)
-                for b_ in ops.MIDM_BUILT:
-                    for s_ in splits:
-                        try:
-                            tim[(b_, s_)] = timeit(lambda i, p=(b_, s_): wide(i, mplan=p), n=20)
-                        except RuntimeError:
-                            pass
-                best = min(tim, key=tim.get)
-                line += (f" | best {best[0]}x{best[1]}={tim[best]:.1f} | " +
-                         " ".join(f"{k[0]}x{k[1]}={v:.1f}" for k, v in sorted(tim.items())))
+                for xd in (1,):
+                    tim = {}
+                    splits = (1,) if proj in ("qkv", "gate_up") else (1, 2, 3, 4, 6, 8)
+                    for b_ in ops.MIDM_BUILT:
+                        for s_ in splits:
+                            try:
+                                tim[(b_, s_)] = timeit(lambda i, p=(b_, s_): wide(i, mplan=p),
+                                                       n=20)
+                            except RuntimeError:
+                                pass
+                    best = min(tim, key=tim.get)
+                    line += (f" | xd{xd} best {best[0]}x{best[1]}={tim[best]:.1f} | " +
+                             " ".join(f"{k[0]}x{k[1]}={v:.1f}" for k, v in sorted(tim.items())))
             if a.sweep:
                 tim = {}
                 for w_ in (4, 6, 7, 8):

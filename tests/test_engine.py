@@ -638,17 +638,19 @@ def test_small_prefill_fused_matches_unfused_and_oracle():
 def test_midm_prefill_engine_matches_oracle(model):
     """Uncached prefill steps of 129-1024 rows run the fused mid-M kernels (ops/csrc/midm.h:
     RMSNorm-folded qkv + RoPE + paged K/V write, o / down residual add with split-K, gate_up
-    + SiLU-mul) inside the engine; teacher-forced greedy tokens against the fp32 dense oracle
-    (near-tie rule), a 400-row first step and a 700-row one."""
+    + SiLU-mul) inside the engine - here forced onto every projection - teacher-forced greedy
+    tokens against the fp32 dense oracle (near-tie rule): 400-, 700- and 190-row steps."""
     vocab = 30000 if model == "small" else 16000
     cfg = EngineConfig(model=model, device="cuda", max_model_len=1024, num_kv_blocks=1024,
                        max_num_batched_tokens=2048, max_num_seqs=8,
                        graph_batch_sizes=(1, 2, 4, 8))
     eng = LLMEngine(cfg)
     m = eng.runner.model
-    assert m.small_prefill_ok(400) and m.small_prefill_ok(700)
+    assert not m.small_prefill_ok(400)
+    assert m.midm_route(400)["qkv"] and m.midm_route(150)["o"] and m.midm_route(600)["down"]
     rng = np.random.default_rng(11)
-    for sizes in ((150, 95, 80, 60, 15), (700,)):
+    m.MIDM_ROUTES = {p: ((129, 1024),) for p in m.MIDM_ROUTES}  # every projection on midm
+    for sizes in ((150, 95, 80, 60, 15), (700,), (190,)):
         prompts = [rng.integers(300, vocab, size=n).tolist() for n in sizes]
         outs, bad = _check(eng, prompts, n=5, tol_logit=0.25)
         assert bad <= max(1, len(prompts) // 2)

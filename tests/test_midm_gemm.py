@@ -92,10 +92,17 @@ def test_midm_gate_up_silu(plan, m, inter, k):
     dt = torch.bfloat16
     x = torch.randn(m, k, dtype=dt, device="cuda")
     w = torch.randn(2 * inter, k, dtype=dt, device="cuda") * 0.02
-    exp = ref.silu_and_mul(torch.nn.functional.linear(_norm_ref(x), w))
+    n = _norm_ref(x)
+    exp = ref.silu_and_mul(torch.nn.functional.linear(n, w))
+    g = n.float() @ w.float().t()
+    o32 = torch.nn.functional.silu(g[:, :inter]) * g[:, inter:]
     ops.set_midm_plan(*plan)
     got = ops.decode_gate_up_silu(x, ops.preshuffle(w, "silu"), 1e-5, preshuffled=True)
-    close(got, exp, 4e-2, 4e-2)
+    # |silu(g) u| reaches ~10 here, where one bf16 rounding of g or u moves the product by
+    # ~0.1: the kernel must be as close to the fp32 oracle as the bf16 library path is
+    e_got = float((got.float() - o32).abs().max())
+    e_ref = float((exp.float() - o32).abs().max())
+    assert e_got <= 1.5 * e_ref + 2e-2, (e_got, e_ref)
 
 
 def test_midm_fp16_and_seam():
