@@ -332,18 +332,23 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
     }
   };
   // each x fragment read from LDS feeds the MFMAs of all TPW tiles of the wave
+  // per K step: the MT fragment reads first, then the MT MFMAs (hipcc otherwise pairs each
+  // read with its MFMA behind an lgkmcnt wait, and the wave idles on LDS latency)
   auto compute = [&](const u32x4 (&f)[NWF], int buf) {
     const unsigned char* b = lds + buf * XBUF + col * kRowB;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int off = ((4 * s + grp) ^ col) << 4;
+      frag8 xf[MT];
 #pragma unroll
-      for (int t = 0; t < MT; ++t) {
-        const frag8 xf = *reinterpret_cast<const frag8*>(b + t * 16 * kRowB + off);
+      for (int t = 0; t < MT; ++t) xf[t] = *reinterpret_cast<const frag8*>(b + t * 16 * kRowB + off);
+#pragma unroll
+      for (int t = 0; t < MT; ++t)
 #pragma unroll
         for (int j = 0; j < TPW; ++j)
-          acc[j][t] = MF::mma(xf, __builtin_bit_cast(frag8, f[j * 4 + s]), acc[j][t]);
-      }
+          acc[j][t] = MF::mma(xf[t], __builtin_bit_cast(frag8, f[j * 4 + s]), acc[j][t]);
+      __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);        // DS read
+      __builtin_amdgcn_sched_group_barrier(0x008, MT * TPW, 0);  // MFMA
     }
   };
   // one chunk: issue chunk c + 2's loads, compute chunk c, stage chunk c + 1's x, barrier.
@@ -354,7 +359,11 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
                   u32x4 (&xload)[PPT], int c, int buf) {
     load_x(xload, min(c + 2, clast));
     load_w(wnext, min(c + kWStages - 1, clast));
+    // the prefetches stay at the chunk head and the LDS writes after the MFMAs (hipcc sank
+    // the loads below the MFMAs, one chunk less of lead on the weight stream)
+    __builtin_amdgcn_sched_barrier(0);
     compute(wcur, buf);
+    __builtin_amdgcn_sched_barrier(0);
     store_x(xstage, buf ^ 1, c + 1 < c1);  // past the end: a re-staged chunk, no squares
     // LDS hand-over only: ds_writes retired, then a bare s_barrier - __syncthreads()' fence
     // semantics made hipcc drain the weight / x loads in flight (vmcnt(0)) at the period's
