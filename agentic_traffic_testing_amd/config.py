@@ -252,6 +252,11 @@ class EngineConfig:
     async_decode: bool = True
     # keep a pre-shuffled copy of the decode-GEMV weights (contiguous 1 KiB wave loads)
     preshuffle_decode_weights: bool = True
+    # GPU engine start: run every tuned library GEMM shape once and serve a few throw-away
+    # requests of the workload's step shapes (prefix cache dropped after), so no code object
+    # (HIP translation unit, rocBLAS / hipBLASLt solution, PyTorch kernel) loads inside a
+    # timed request (bench/coldstart.py: first 560-row prefill 1157 ms -> 11.5 ms without)
+    startup_warmup: bool = True
     # "" = 16-bit weights; "fp8" = OCP e4m3fn weight-only quantisation with per-row scales
     # (decode: fp8 GEMV kernels; prefill: hipBLASLt fp8 GEMM) - BASELINE config 5
     quantization: str = ""

@@ -144,6 +144,8 @@ class ModelRunner:
             ops.ensure_splitk_workspace(self.device)
             if cfg.fused_decode:
                 ops.warm_wide_kernels(self.device, self.dtype)
+            if cfg.startup_warmup:
+                self.warm_library_gemms()
         self.block_size = cfg.block_size
         self.bt_width = math.ceil(cfg.max_model_len / cfg.block_size)
         self.part_tokens = cfg.decode_partition_tokens
@@ -720,6 +722,46 @@ class ModelRunner:
             for p in (buckets if all_parts else [top]):
                 if (b, p, 0) not in self.graphs:
                     self.capture(b, p)
+
+    def warm_library_gemms(self) -> int:
+        """Run every shape of the loaded TunableOp table that this rank's weights have once
+        (bf16: plain and residual-add GEMM; fp8: the row-scaled GEMM), so each rocBLAS /
+        hipBLASLt solution's code object - and the libraries themselves - load at engine
+        start, not inside the first request of that bucket (rocBLAS initialisation alone put
+        ~1.1 s into the first 560-row prefill, bench/coldstart.py).  Returns the GEMMs run."""
+        if self.gemm_table is None or not self.is_cuda or not self.model.layers:
+            return 0
+        import re
+
+        L = self.model.layers[0]
+        ws = {}
+        for name in ("qkv", "o", "gate_up", "down"):
+            w = getattr(L, name)
+            ws[tuple(w.shape)] = (w, getattr(L, name + "_s"))
+        ws.setdefault(tuple(self.model.lm_head.shape), (self.model.lm_head, None))
+        pat = re.compile(r"^(\w+?)_TN,tn_(\d+)_(\d+)_(\d+)_")
+        n = 0
+        with open(self.gemm_table) as f, torch.inference_mode():
+            for line in f:
+                mt = pat.match(line)
+                if mt is None:
+                    continue
+                op, N, M, K = mt.group(1), int(mt.group(2)), int(mt.group(3)), int(mt.group(4))
+                w, s = ws.get((N, K), (None, None))
+                if w is None:
+                    continue
+                if op.startswith("ScaledGemm") and s is not None:
+                    xq = torch.zeros(M, K, dtype=torch.uint8, device=self.device)
+                    ops.gemm_fp8(xq, torch.ones(M, 1, device=self.device), w, s, self.dtype)
+                elif op.startswith("GemmTunableOp") and s is None and w.dtype == self.dtype:
+                    x = torch.zeros(M, K, dtype=w.dtype, device=self.device)
+                    torch.nn.functional.linear(x, w)
+                    torch.zeros(M, N, dtype=w.dtype, device=self.device).addmm_(x, w.t())
+                else:
+                    continue
+                n += 1
+        torch.cuda.synchronize(self.device)
+        return n
 
     def reset_state(self):
         """Drop prefix cache contents (used between benchmark phases)."""

@@ -343,7 +343,7 @@ class LlamaModel:
             if small or mid.get("qkv"):
                 q = ops.decode_qkv_rope(residual, L.qkv_ps if ps else L.qkv, eps, md.positions,
                                         md.slot_mapping, self.cos_sin, k_caches[li],
-                                        v_caches[li], nq, nkv, preshuffled=ps)
+                                        v_caches[li], nq, nkv, preshuffled=ps, w_scale=L.qkv_s)
             else:
                 if fp8:
                     if pending is None:
@@ -367,7 +367,7 @@ class LlamaModel:
                 ops.attention_prefill(q, k_caches[li], v_caches[li], md.block_tables,
                                       md.seq_kvlen, md.seq_qstart, md.tile_seq, md.tile_qoff,
                                       self.scale, out=attn)
-            if fp8:
+            if fp8 and not small:
                 aq, as_ = ops.quant_rows_fp8(attn.view(T, nq * D))
                 y = self._all_reduce(self._gemm8(aq, as_, L.o, L.o_s, dt, "o"))
                 xq, xs = ops.quant_rows_fp8(y, ops.QUANT_ADDNORM, L.post_norm, eps, residual)
@@ -381,14 +381,12 @@ class LlamaModel:
                 pending = self._all_reduce(self._gemm8(aq, as_, L.down, L.down_s, dt, "down"))
                 continue
             if small or mid.get("o"):
-                ops.linear(attn.view(T, nq * D), L.o_ps if ps else L.o, residual=residual,
-                           waves=ops.decode_waves("o", ps, False), preshuffled=ps, ksplit=None,
-                           proj="o")
+                self._row_parallel(attn.view(T, nq * D), L, "o", residual)
             else:
                 self._proj_residual(attn.view(T, nq * D), L.o, L.o_s, residual, "o")
             if small or mid.get("gate_up"):
                 a = ops.decode_gate_up_silu(residual, L.gate_up_ps if ps else L.gate_up, eps,
-                                            preshuffled=ps)
+                                            preshuffled=ps, w_scale=L.gate_up_s)
             else:
                 x = ops.rms_norm(residual, L.post_norm, eps)
                 if self._pg(T, L.gate_up, mode=ops.GEMM_SILU, proj="gate_up"):
@@ -397,9 +395,7 @@ class LlamaModel:
                     gu = self._proj(x, L.gate_up, L.gate_up_s)
                     a = ops.silu_and_mul(gu)
             if small or mid.get("down"):
-                ops.linear(a, L.down_ps if ps else L.down, residual=residual,
-                           waves=ops.decode_waves("down", ps, False), preshuffled=ps,
-                           ksplit=None, proj="down")
+                self._row_parallel(a, L, "down", residual)
             else:
                 self._proj_residual(a, L.down, L.down_s, residual, "down")
         if rows is not None:
@@ -506,18 +502,21 @@ class LlamaModel:
         """Does a (prefill or mixed) step of T rows run on the fused decode kernels - RMSNorm
         folded into the pre-shuffled skinny GEMVs, RoPE + KV write in the QKV epilogue, SiLU-mul
         in gate_up?  The one predicate for forward() and the runner's row padding (ADVICE r4:
-        TP / fp8 steps of <= 32 rows take the library path and must be padded to its tuned
-        buckets; fused_decode=False turns the fused kernels off here too).  Up to 128 rows:
-        past that every projection is routed on its own (midm_route)."""
+        steps that take the library path are padded to its tuned buckets; fused_decode=False
+        turns the fused kernels off here too).  Up to 128 rows, 16-bit or fp8 weights, any TP
+        degree (the row-parallel sums go through _row_parallel); past 128 rows every
+        projection is routed on its own (midm_route)."""
         return (self.small_prefill_fused and self.fused_decode and self.device.type == "cuda"
-                and self.tp_size == 1 and self.quant != "fp8" and T <= 128
-                and self.decode_fusable(T))
+                and T <= 128 and self.decode_fusable(T)
+                and (self.quant != "fp8" or (bool(self.layers)
+                                             and self.layers[0].qkv_ps is not None)))
 
     def decode_fusable(self, num_tokens: int) -> bool:
         """Can a step of this many rows run the fused weight-streaming kernels?  <= 32 rows:
-        the 16-row-tile GEMVs (any layout); 33..128 rows: the wide small-M kernel; 129..
-        ops.MIDM_MAX_M rows: the mid-M kernel - both over the pre-shuffled 16-bit weights
-        (TP=1: the TP decode step's push / one-shot collectives are sized for <= 32 rows)."""
+        the 16-row-tile GEMVs (any layout); 33..128 rows: the wide small-M kernel over the
+        pre-shuffled 16-bit or fp8 weights (any TP degree: past the fused push's 32 rows the
+        row-parallel sums take the IPC / RCCL all-reduce); 129..ops.MIDM_MAX_M rows: the mid-M
+        kernel (16-bit weights, TP = 1)."""
         # 16-bit GEMVs: K % 128 (4 waves x 32); fp8 GEMVs: K % 256 (4 waves x 64)
         step = 256 if self.quant == "fp8" else 128
         dims = (self.device.type == "cuda" and self.cfg.hidden_size % step == 0
@@ -526,9 +525,10 @@ class LlamaModel:
             return False
         if num_tokens <= ops.SKINNY_MAX_M:
             return True
-        return (num_tokens <= ops.fused_max_rows(True, self.quant == "fp8")
-                and self.quant != "fp8" and self.tp_size == 1
-                and bool(self.layers) and self.layers[0].qkv_ps is not None
+        lim = ops.fused_max_rows(True, self.quant == "fp8")
+        if self.tp_size > 1:
+            lim = min(lim, 128)  # the mid-M routes are measured at TP = 1 shapes only
+        return (num_tokens <= lim and bool(self.layers) and self.layers[0].qkv_ps is not None
                 and self.lm_head_ps is not None)
 
     def hidden_fusable(self) -> bool:
@@ -565,42 +565,37 @@ class LlamaModel:
                                     md.seq_kvlen, md.seq_qstart, self.scale, ws["part_out"],
                                     ws["part_lse"], ws["counters"], ws["max_parts"],
                                     ws["part_tokens"], out=attn, num_seqs=B)
-            a2 = attn.view(B, nq * self.head_dim)
-            if self.tp_size == 1:
-                ops.linear(a2, L.o_ps if ps else L.o, residual=residual,
-                           waves=ops.decode_waves("o", ps, L.o_s is not None),
-                           preshuffled=ps, w_scale=L.o_s, ksplit=None, proj="o")
-            elif self.tp_group.push_ok(B, L.o.shape[0]):
-                # X1: the GEMV epilogue pushes into the peers' slots; one receive kernel
-                # adds the rank-order sum into the residual (no standalone one-shot kernel)
-                ops.linear_push_reduce(a2, L.o_ps if ps else L.o, residual, self.tp_group.ipc,
-                                       waves=ops.decode_waves("o", ps, L.o_s is not None),
-                                       preshuffled=ps, w_scale=L.o_s, proj="o")
-            else:
-                self.tp_group.all_reduce_residual(
-                    ops.linear(a2, L.o_ps if ps else L.o, preshuffled=ps, w_scale=L.o_s,
-                               ksplit=None, proj="o"), residual)
+            self._row_parallel(attn.view(B, nq * self.head_dim), L, "o", residual)
             ops.decode_gate_up_silu(residual, L.gate_up_ps if ps else L.gate_up, eps, out=act,
                                     preshuffled=ps, w_scale=L.gate_up_s)
-            if self.tp_size == 1:
-                ops.linear(act, L.down_ps if ps else L.down, residual=residual,
-                           waves=ops.decode_waves("down", ps, L.down_s is not None),
-                           preshuffled=ps, w_scale=L.down_s, ksplit=None,
-                           proj="down")
-            elif self.tp_group.push_ok(B, L.down.shape[0]):
-                ops.linear_push_reduce(act, L.down_ps if ps else L.down, residual,
-                                       self.tp_group.ipc,
-                                       waves=ops.decode_waves("down", ps, L.down_s is not None),
-                                       preshuffled=ps, w_scale=L.down_s, proj="down")
-            else:
-                self.tp_group.all_reduce_residual(
-                    ops.linear(act, L.down_ps if ps else L.down, preshuffled=ps,
-                               w_scale=L.down_s, ksplit=None, proj="down"), residual)
+            self._row_parallel(act, L, "down", residual)
         if top_p is not None:
             logits = self.compute_logits(ops.rms_norm(residual, self.norm, eps))
             return ops.sample_topkp(logits, temperature, top_p, top_k, seeds, steps,
                                     out=ws["tokens"][:B])
         return self.sample_rows(residual, eps, temperature, seeds, steps, ws)
+
+    def _row_parallel(self, x: torch.Tensor, L, proj: str, residual: torch.Tensor) -> None:
+        """residual += x @ W.T for the row-parallel o / down projection on the fused kernels
+        (16-row-tile GEMV, wide or mid-M kernel; fp8 weights with their row scales).  TP: the
+        GEMV epilogue pushes the partial product into the peers' IPC slots and one receive
+        kernel adds the rank-order sum into the residual (X1 / X2, <= 32 rows), else the
+        product goes through the all-reduce whose epilogue adds it (IPC one- / two-shot, or
+        RCCL)."""
+        ps = L.qkv_ps is not None
+        w = getattr(L, proj + "_ps") if ps else getattr(L, proj)
+        scale = getattr(L, proj + "_s")
+        waves = ops.decode_waves(proj, ps, scale is not None)
+        if self.tp_size == 1:
+            ops.linear(x, w, residual=residual, waves=waves, preshuffled=ps, w_scale=scale,
+                       ksplit=None, proj=proj)
+        elif self.tp_group.push_ok(x.shape[0], w.shape[0]):
+            ops.linear_push_reduce(x, w, residual, self.tp_group.ipc, waves=waves,
+                                   preshuffled=ps, w_scale=scale, proj=proj)
+        else:
+            self.tp_group.all_reduce_residual(
+                ops.linear(x, w, waves=waves, preshuffled=ps, w_scale=scale, ksplit=None,
+                           proj=proj), residual)
 
     def sample_rows(self, x, eps, temperature, seeds, steps, ws) -> torch.Tensor:
         """[final RMSNorm (eps > 0) +] LM head + sampler for <= 32 rows without materialising

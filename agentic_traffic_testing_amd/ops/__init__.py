@@ -340,9 +340,13 @@ MIDM_MAX_M = int(os.environ.get("ATTA_MIDM_MAX_M", "1024"))
 
 def fused_max_rows(preshuffled: bool = True, fp8: bool = False) -> int:
     """Most rows a call may have to run on the hand-written weight-streaming kernels (the
-    16-row-tile GEMVs, the wide small-M kernel, the mid-M kernel) for this weight format."""
-    if not preshuffled or fp8 or WIDE_MAX_M <= SKINNY_MAX_M:
+    16-row-tile GEMVs, the wide small-M kernel, the mid-M kernel) for this weight format:
+    pre-shuffled fp8 weights run the wide kernel's W8 builds up to 128 rows (the mid-M kernel
+    is 16-bit only)."""
+    if not preshuffled or WIDE_MAX_M <= SKINNY_MAX_M:
         return SKINNY_MAX_M
+    if fp8:
+        return min(WIDE_MAX_M, 128)
     if WIDE_MAX_M >= 128 and MIDM_MAX_M > 128:
         return MIDM_MAX_M
     return min(WIDE_MAX_M, 128)

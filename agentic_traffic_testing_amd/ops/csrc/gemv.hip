@@ -219,6 +219,11 @@ void atta_get_wide_min_rows(int* m, int* m_silu) {
 }
 // pre-shuffled 16-bit calls of up to this many rows run the wide (<= 128) or mid-M kernels
 constexpr int kMidmMaxM = 8192;
+// rows one call may carry: row-major weights the 16-row-tile GEMV (<= 32); pre-shuffled fp8
+// weights also the wide kernel's W8 builds (<= 128); pre-shuffled 16-bit the mid-M kernel too
+static int max_rows(int ps, const float* wscale) {
+  return !ps ? 32 : (wscale != nullptr ? 128 : kMidmMaxM);
+}
 static bool use_wide(int M, int ps, const float* wscale, bool silu = false) {
   return M > 32 ||
          (ps && wscale == nullptr && M >= (silu ? g_wide_min_m_silu : g_wide_min_m));
@@ -253,7 +258,9 @@ static int wide(SkinnyParams& p, int epi, int ntiles, int dtype, hipStream_t str
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -2;
   const SplitKWs& w = g_splitk[dev];
   if (p.M > 128) {
-    // past the wide kernel's 8 row blocks: the mid-M kernel (midm.hip, row-blocked grid)
+    // past the wide kernel's 8 row blocks: the mid-M kernel (midm.hip, row-blocked grid;
+    // 16-bit weights only)
+    if (p.wscale != nullptr) return -1;
     p.wg_trace = nullptr;
     return atta_midm_launch(p, epi, ntiles, dtype, w.ws, w.ws_floats, stream);
   }
@@ -292,7 +299,7 @@ int atta_skinny_gemm(void* y, const void* x, const void* w, const void* residual
                      int ksplit, const float* wscale, int dtype, hipStream_t stream) {
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
-  if (M < 1 || M > (ps && wscale == nullptr ? kMidmMaxM : 32) || N % 16 != 0) return -1;
+  if (M < 1 || M > max_rows(ps, wscale) || N % 16 != 0) return -1;
   SkinnyParams p{};
   p.ps = ps;
   p.wscale = wscale;
@@ -370,7 +377,7 @@ int atta_fused_qkv_rope(void* q_out, void* k_cache, void* v_cache, const void* x
                         int dtype, hipStream_t stream) {
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
-  if (M < 1 || M > (ps && wscale == nullptr ? kMidmMaxM : 32)) return -1;
+  if (M < 1 || M > max_rows(ps, wscale)) return -1;
   int shift = 0;
   while ((1 << shift) < block_size) ++shift;
   if ((1 << shift) != block_size) return -1;
@@ -407,7 +414,7 @@ int atta_fused_gate_up_silu(void* out, const void* x, const void* w, int M, int 
                             int ksplit, const float* wscale, int dtype, hipStream_t stream) {
   const int ps = (dtype & kPreshuffled) ? 1 : 0;
   dtype &= ~kPreshuffled;
-  if (M < 1 || M > (ps && wscale == nullptr ? kMidmMaxM : 32) || inter % 8 != 0) return -1;
+  if (M < 1 || M > max_rows(ps, wscale) || inter % 8 != 0) return -1;
   SkinnyParams p{};
   p.ps = ps;
   p.wscale = wscale;

@@ -229,7 +229,11 @@ __device__ __forceinline__ void epi_apply(const SkinnyParams& p, const int tile,
   }
 }
 
-template <typename T, int WAVES, int MT, int EPI, bool NORM, int TPW>
+// W8: fp8 (e4m3fn) weights in the skinny GEMV's 16-row x 64-K blocks of 1 KiB (skinny.h), two
+// 16-byte loads per tile per chunk instead of four, converted to 16-bit MFMA operands in
+// registers (v_cvt_scalef32_pk_*_fp8) and the per-row dequant scale applied to the finished
+// accumulators: weight-only quantisation, the activations stay 16-bit (no per-token quant pass)
+template <typename T, int WAVES, int MT, int EPI, bool NORM, int TPW, bool W8 = false>
 __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int ntiles) {
   using MF = MfmaK32<T>;
   using frag8 = typename MF::frag8;
@@ -262,15 +266,19 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
   constexpr bool norm = NORM;  // p.eps > 0: fused RMSNorm (compile-time: no branches in the loop)
   // weight register stages (chunks of weights in flight + 1): 4 x one tile, 3 x two tiles
   constexpr int kWStages = TPW == 1 ? kDeepW : 3;
-  constexpr int NWF = TPW * 4;  // weight fragments per chunk per wave
+  constexpr int NW = W8 ? 2 : 4;  // 16-B weight loads per tile per chunk
+  constexpr int NWF = TPW * NW;   // weight registers (u32x4) per chunk per wave
 
   // this wave's weight tiles (idle tiles of the last column block stream tile 0 and store
   // nothing: every wave takes part in the barriers)
-  const uint16_t* wp[TPW];
+  // (byte pointers: a tile's pre-shuffled weights are K / 32 (16-bit) or K / 64 (fp8) 1 KiB
+  // blocks, chunk c's are blocks c * NW .. c * NW + NW - 1)
+  const unsigned char* wp[TPW];
 #pragma unroll
   for (int j = 0; j < TPW; ++j)
-    wp[j] = p.w + static_cast<int64_t>(tile0 + j < ntiles ? tile0 + j : 0) * (p.K / 32) * 512 +
-            lane * 8;
+    wp[j] = reinterpret_cast<const unsigned char*>(p.w) +
+            static_cast<int64_t>(tile0 + j < ntiles ? tile0 + j : 0) * (p.K / (W8 ? 64 : 32)) * 1024 +
+            lane * 16;
   // x pieces of this thread: piece q = tid + i * NTHR -> staged row q / 16, slot q % 16
   int xsrc[PPT];  // element offsets from p.x (32-bit: x is < 4 MB here)
   int xdst[PPT];
@@ -305,9 +313,9 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
 #pragma unroll
     for (int j = 0; j < TPW; ++j)
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        f[j * 4 + s] =
-            __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wp[j] + (c * 4 + s) * 512));
+      for (int s = 0; s < NW; ++s)
+        f[j * NW + s] =
+            __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wp[j] + (c * NW + s) * 1024));
   };
   auto load_x = [&](u32x4 (&xr)[PPT], int c) {
 #pragma unroll
@@ -336,6 +344,19 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
   // read with its MFMA behind an lgkmcnt wait, and the wave idles on LDS latency)
   auto compute = [&](const u32x4 (&f)[NWF], int buf) {
     const unsigned char* b = lds + buf * XBUF + col * kRowB;
+    // weight fragment of tile j, K step s (fp8: converted up front, outside the MFMA groups)
+    frag8 wf[TPW][4];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        if constexpr (W8) {
+          const u32x4 r = f[j * 2 + (s >> 1)];
+          wf[j][s] = (s & 1) ? fp8x8_to_frag<T>(r[2], r[3]) : fp8x8_to_frag<T>(r[0], r[1]);
+        } else {
+          wf[j][s] = __builtin_bit_cast(frag8, f[j * 4 + s]);
+        }
+      }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int off = ((4 * s + grp) ^ col) << 4;
@@ -346,7 +367,7 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
       for (int t = 0; t < MT; ++t)
 #pragma unroll
         for (int j = 0; j < TPW; ++j)
-          acc[j][t] = MF::mma(xf[t], __builtin_bit_cast(frag8, f[j * 4 + s]), acc[j][t]);
+          acc[j][t] = MF::mma(xf[t], wf[j][s], acc[j][t]);
       __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);        // DS read
       __builtin_amdgcn_sched_group_barrier(0x008, MT * TPW, 0);  // MFMA
     }
@@ -426,6 +447,18 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
   }
 
   if (p.wg_trace != nullptr) tr1 = tr2 = wall_clock64();
+  if constexpr (W8) {
+    // dequant: lane column col of tile j is weight row tile_row(tile, col) (split-K slices
+    // publish scaled partials - the sum is linear)
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      const float sc = p.wscale[tile_row<EPI>(tile0 + j < ntiles ? tile0 + j : 0, col, p)];
+#pragma unroll
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[j][t][i] *= sc;
+    }
+  }
   // ---- row sums of squares: the 16 lanes staging one row are consecutive -------------------
   if (norm) {
 #pragma unroll
@@ -525,9 +558,40 @@ constexpr bool tpw2_built(int waves) { return waves == 4 || waves == 8; }
 // projections (x is already the attention / SiLU output), always for qkv and gate_up (eps > 0),
 // either way for the LM-head sampler (decode: final norm fused; prefill rows: already normed)
 template <typename T, int WAVES, int MT, int TPW>
+inline int launch_epi_w8(int epi, dim3 grid, hipStream_t st, const SkinnyParams& p, int ntiles) {
+  const dim3 blk(WAVES * 64);
+  const bool norm = p.eps > 0.f;
+  switch (epi) {
+    case EPI_PLAIN:
+      if (norm) return -1;
+      wide_kernel<T, WAVES, MT, EPI_PLAIN, false, TPW, true><<<grid, blk, 0, st>>>(p, ntiles);
+      return 0;
+    case EPI_RESADD:
+      if (norm) return -1;
+      wide_kernel<T, WAVES, MT, EPI_RESADD, false, TPW, true><<<grid, blk, 0, st>>>(p, ntiles);
+      return 0;
+    case EPI_QKVROPE:
+      if (!norm) return -1;
+      wide_kernel<T, WAVES, MT, EPI_QKVROPE, true, TPW, true><<<grid, blk, 0, st>>>(p, ntiles);
+      return 0;
+    case EPI_SILU:
+      if (!norm) return -1;
+      wide_kernel<T, WAVES, MT, EPI_SILU, true, TPW, true><<<grid, blk, 0, st>>>(p, ntiles);
+      return 0;
+    default: return -1;  // the LM head stays 16-bit
+  }
+}
+
+template <typename T, int WAVES, int MT, int TPW>
 inline int launch_epi(int epi, dim3 grid, hipStream_t st, const SkinnyParams& p, int ntiles) {
   const dim3 blk(WAVES * 64);
   const bool norm = p.eps > 0.f;
+  if (p.wscale != nullptr) {
+    // fp8 weights: built for 4 and 8 waves (the plan offers only those)
+    if constexpr ((WAVES == 4 || WAVES == 8) && TPW == 1)
+      return launch_epi_w8<T, WAVES, MT, TPW>(epi, grid, st, p, ntiles);
+    return -1;
+  }
   constexpr bool kNormOk = norm_fits(WAVES, MT, TPW);
   if constexpr (!kNormOk) {
     if (norm) return -1;

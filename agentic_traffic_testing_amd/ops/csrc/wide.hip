@@ -128,7 +128,8 @@ static double env_or(const char* name, double dflt) {
   return v != nullptr ? std::atof(v) : dflt;
 }
 
-static void plan(int ntiles, int K, int M, bool norm, int& waves, int& tpw, int& ksplit) {
+static void plan(int ntiles, int K, int M, bool norm, bool w8, int& waves, int& tpw,
+                 int& ksplit) {
   constexpr double kCUs = 256.0, kBpus = 24e3;  // bytes per us per CU
   // cost-model knobs (env overrides for A/B runs; read once)
   static const double kXDiv = env_or("ATTA_WIDE_PLAN_XDIV", 6.0);
@@ -141,13 +142,14 @@ static void plan(int ntiles, int K, int M, bool norm, int& waves, int& tpw, int&
     for (int wi = 0; wi < 4; ++wi) {
       const int w = ws[wi];
       if (norm && !norm_fits(w, (M + 15) / 16, tp)) continue;  // see launch_epi
+      if (w8 && w != 4 && w != 8) continue;                     // fp8 builds (launch_epi)
       if (tp == 2 && !tpw2_built(w)) continue;
       const int tb = w * tp;
       const int ncb = (ntiles + tb - 1) / tb;
       for (int s = 1; s <= 8 && nch / s >= 2; ++s) {
         const double rounds = std::ceil(ncb * s / kCUs);
         const double kslice = static_cast<double>(K) / s;
-        const double bytes = tb * 16.0 * kslice * 2.0 + mpad * kslice * 2.0 / kXDiv;
+        const double bytes = tb * 16.0 * kslice * (w8 ? 1.0 : 2.0) + mpad * kslice * 2.0 / kXDiv;
         const double idle = static_cast<double>(ncb * tb - ntiles) / (ncb * tb);  // empty tiles
         // split: a reduce launch (~1 us beyond the slabs it reads) reading every slice's slab;
         // x bytes at 1/6 and the 1 us fitted to the round-5 graph-mode sweep
@@ -178,7 +180,8 @@ using namespace atta;
 int atta_wide_launch(SkinnyParams& p, int epi, int ntiles, int waves, int ksplit, int dtype,
                      const float* sk_ws, int* sk_counters, int64_t ws_floats, int n_counters,
                      hipStream_t stream) {
-  if (p.M < 1 || p.M > 128 || p.K % wide::kKC != 0 || !p.ps || p.wscale != nullptr) return -1;
+  if (p.M < 1 || p.M > 128 || p.K % wide::kKC != 0 || !p.ps) return -1;
+  const bool w8 = p.wscale != nullptr;  // fp8 weights (W8 builds: 4 / 8 waves)
   // waves 14 / 16 / 17 / 18 in an explicit plan = 4 / 6 / 7 / 8 waves x two tiles per wave
   // (measured slower and not built: such a plan returns -1 from the launcher)
   int tpw = 1;
@@ -186,7 +189,8 @@ int atta_wide_launch(SkinnyParams& p, int epi, int ntiles, int waves, int ksplit
     tpw = 2;
     waves -= 10;
   }
-  if (waves <= 0 || ksplit <= 0) wide::plan(ntiles, p.K, p.M, p.eps > 0.f, waves, tpw, ksplit);
+  if (waves <= 0 || ksplit <= 0)
+    wide::plan(ntiles, p.K, p.M, p.eps > 0.f, w8, waves, tpw, ksplit);
   if (waves != 4 && waves != 6 && waves != 7 && waves != 8) return -1;
   if (ksplit < 1 || p.K / wide::kKC < ksplit) return -1;
   // 16-row blocks: rows padded to the next 16 only (75 rows: 80, not 96)

@@ -64,7 +64,7 @@ class TPComm:
         """Can a row-parallel decode GEMV push its product straight into the peers'
         receive slots (IPC path, fused push)?"""
         return (self.size > 1 and self.ipc is not None and self.fused_push
-                and self.ipc.push_eligible(rows, n_out))
+                and rows <= 32 and self.ipc.push_eligible(rows, n_out))  # GEMV: <= 32 rows
 
     fused_push: bool = True
 

@@ -148,10 +148,13 @@ class TPEngine(LLMEngine):
                                   world - 1, create=True,
                                   register_timeout_s=cfg.tp_register_timeout_s)
         runner.publisher = self.channel
+        self._defer_warmup = True
         super().__init__(cfg, runner=runner, device=device)
         self._closed = False
         try:
             runner.capture_all()
+            if cfg.startup_warmup and runner.is_cuda:
+                self.warmup()
         except BaseException:
             self.kill()
             raise

@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 import torch
 
+from agentic_traffic_testing_amd import ops
 from agentic_traffic_testing_amd.config import EngineConfig
 from agentic_traffic_testing_amd.engine.llm_engine import LLMEngine
 from agentic_traffic_testing_amd.engine.sequence import SamplingParams
@@ -404,17 +405,20 @@ def test_tp_fp8_same_gpu_graph_captured_decode(tp):
         assert r.graph_steps - g0 >= 0.95 * decode_steps, (r.graph_steps - g0, decode_steps)
         ipc = eng.comm.ipc
         assert ipc.calls_push > 0 and ipc.check() == 0
+        eng_fused = r.model.small_prefill_ok(sum(len(p) for p in _prompts()))
     finally:
         eng.shutdown()
     # teacher-forced against the oracle (random-init weights make near ties common, and one
     # flip changes every later token of a sequence, so sequence equality with TP=1 is not
-    # required; the TP=1 fp8 prefill itself quantises activations per token, ~0.5 logit off
-    # the weight-only oracle at the first token)
+    # required).  The 112-row prefill runs the fused weight-only kernels (wide W8 builds:
+    # 16-bit activations, like decode); a library-path prefill would quantise its activations
+    # per token, which the oracle then mirrors on the prompt rows
+    fused = eng_fused
     bad_pos = checked = 0
     for p, g in zip(_prompts(), got):
         ids = list(p)
         for t in g:
-            lg = dense_logits_fp8(m1, ids, len(p))
+            lg = dense_logits_fp8(m1, ids, 0 if fused else len(p))
             checked += 1
             if int(torch.argmax(lg)) != t:
                 gap = float(lg.max() - lg[t])
@@ -587,3 +591,56 @@ def test_ipc_allreduce_ranks_one_gpu(world):
     for rank, bad, calls in res:
         assert bad == [], bad
         assert calls > 20
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tp", [1, 8])
+def test_fp8_fused_past_32_rows_prefill_and_decode(tp):
+    """fp8 weights (BASELINE config 5) on the fused kernels past 32 rows, TP=1
+    and a same-GPU TP=8 rehearsal on the 70B per-rank geometry: one 100-row prefill step of 48
+    sequences (wide kernel W8 builds: norm fold + RoPE / KV write, SiLU-mul, and o / down whose
+    partial sums take the IPC all-reduce - past the fused push's 32 rows) and B=48 decode steps
+    replayed from hipGraphs.  Tokens teacher-forced against the fp32 oracle of the dequantised
+    weights with 16-bit activations (weight-only, like the kernels), near-tie rule."""
+    from helpers import dense_logits_fp8
+
+    rng = np.random.default_rng(17)
+    prompts = [rng.integers(300, 3000, size=n).tolist() for n in [2] * 44 + [3] * 4]
+    base = dict(model="llama-70b-tp-slice-fp8", device="cuda:0", max_model_len=256,
+                num_kv_blocks=256, max_num_batched_tokens=512, max_num_seqs=48,
+                graph_batch_sizes=(1, 8, 48), use_graphs=True, quantization="fp8")
+    greedy = SamplingParams(temperature=0.0, max_tokens=6, ignore_eos=True)
+    ref_eng = LLMEngine(EngineConfig(**base))
+    m1 = ref_eng.runner.model
+    if tp == 1:
+        eng = ref_eng
+    else:
+        eng = TPEngine(EngineConfig(tensor_parallel_size=tp, tp_same_device=True,
+                                    tp_allreduce="ipc", tp_fused_push=True, **base))
+    try:
+        r = eng.runner
+        m = r.model
+        assert m.quant == "fp8" and m.small_prefill_ok(100) and m.decode_fusable(48)
+        assert not m.midm_route(100) and ops.fused_max_rows(True, True) == 128
+        steps0, g0 = r.steps, r.graph_steps
+        got = [o.token_ids for o in eng.generate(prompts, greedy)]
+        assert all(len(g) == 6 for g in got)
+        decode_steps = r.steps - steps0 - 1
+        assert r.graph_steps - g0 >= 0.8 * decode_steps, (r.graph_steps - g0, decode_steps)
+        if tp > 1:
+            assert eng.comm.ipc.check() == 0
+    finally:
+        if tp > 1:
+            eng.shutdown()
+    bad_pos = checked = 0
+    for p, g in list(zip(prompts, got))[::4]:
+        ids = list(p)
+        for t in g:
+            lg = dense_logits_fp8(m1, ids, 0)
+            checked += 1
+            if int(torch.argmax(lg)) != t:
+                gap = float(lg.max() - lg[t])
+                assert gap < 0.3, (g, len(ids) - len(p), gap)
+                bad_pos += 1
+            ids.append(t)
+    assert bad_pos <= checked // 5, (bad_pos, checked)

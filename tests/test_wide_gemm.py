@@ -152,3 +152,91 @@ def test_wide_matches_skinny_at_the_seam():
     a = ops.linear(x[:32].contiguous(), wp, preshuffled=True)
     b = ops.linear(x, wp, preshuffled=True)
     close(b[:32], a, 2e-2, 1e-2)
+
+
+# ---- fp8 weights (W8 builds: e4m3fn weight-only quantisation, per-row scales) ----------------
+W8_PLANS = [(0, 0), (4, 1), (8, 1), (8, 3), (4, 5)]
+
+
+def _fp8(w, rowmap="plain"):
+    """(pre-shuffled fp8 bytes, row scales, the dequantised fp32 weight the oracle uses)."""
+    q, s = ops.quantize_fp8(w)
+    deq = q.view(torch.float8_e4m3fn).float() * s[:, None]
+    return ops.preshuffle_fp8(q, rowmap), s, deq
+
+
+@pytest.mark.parametrize("plan", W8_PLANS)
+@pytest.mark.parametrize("m,n,k", [(33, 1024, 4096), (85, 4096, 4096), (128, 512, 14336),
+                                   (47, 6144, 1024), (100, 2048, 2048)])
+def test_wide_fp8_linear_plain_and_residual(plan, m, n, k):
+    """33-128 rows over fp8 weights: the wide kernel's W8 builds (weights converted to bf16
+    MFMA operands in registers, the row scale on the finished accumulators) against the fp32
+    product with the dequantised weights; split-K plans deterministic."""
+    torch.manual_seed(46)
+    dt = torch.bfloat16
+    x = torch.randn(m, k, dtype=dt, device="cuda")
+    wq, s, deq = _fp8(torch.randn(n, k, dtype=dt, device="cuda") * 0.02)
+    exp = x.float() @ deq.t()
+    assert ops.skinny_ok(x, wq, preshuffled=True, fp8=True)
+    ops.set_wide_plan(*plan)
+    got = ops.linear(x, wq, w_scale=s)
+    close(got, exp, 2e-2 * math.sqrt(k / 4096), 1e-2)
+    r = torch.randn(m, n, dtype=dt, device="cuda")
+    exp_r = exp.to(dt).float() + r.float()
+    ops.set_wide_plan(*plan)
+    ops.linear(x, wq, residual=r, w_scale=s)
+    close(r, exp_r, 3e-2 * math.sqrt(k / 4096), 1e-2)
+    ops.set_wide_plan(*plan)
+    a = ops.linear(x, wq, w_scale=s)
+    ops.set_wide_plan(*plan)
+    b = ops.linear(x, wq, w_scale=s)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("plan", [(0, 0), (8, 1), (4, 3)])
+@pytest.mark.parametrize("m", [33, 75, 128])
+def test_wide_fp8_qkv_rope(plan, m):
+    torch.manual_seed(47)
+    dt, bs, nb, hq, hkv, H = torch.bfloat16, 16, 64, 8, 1, 8192
+    x = torch.randn(m, H, dtype=dt, device="cuda") * 2
+    wq, s, deq = _fp8(torch.randn((hq + 2 * hkv) * 128, H, dtype=dt, device="cuda") * 0.02,
+                      "qkv")
+    pos = torch.randint(0, 4000, (m,), dtype=torch.int32, device="cuda")
+    slots = torch.randperm(nb * bs, device="cuda")[:m].to(torch.int32)
+    slots[1] = -1
+    cs = ref.rope_cos_sin(128, 8192, 500000.0, None, device="cuda")
+    k1 = torch.randn(nb, hkv, bs, 128, dtype=dt, device="cuda")
+    v1 = torch.randn(nb, hkv, 128, bs, dtype=dt, device="cuda")
+    k2, v2 = k1.clone(), v1.clone()
+    q_exp = ref.rope_cache(torch.nn.functional.linear(_norm_ref(x).float(), deq).to(dt), pos,
+                           slots, cs, k1, v1, hq, hkv, 128)
+    ops.set_wide_plan(*plan)
+    q_got = ops.decode_qkv_rope(x, wq, 1e-5, pos, slots, cs, k2, v2, hq, hkv, w_scale=s)
+    close(q_got, q_exp, 3e-2, 2e-2)
+    close(k2, k1, 3e-2, 2e-2)
+    close(v2, v1, 3e-2, 2e-2)
+
+
+@pytest.mark.parametrize("plan", [(0, 0), (8, 2), (4, 1)])
+@pytest.mark.parametrize("m", [33, 85, 128])
+def test_wide_fp8_gate_up_silu(plan, m):
+    torch.manual_seed(48)
+    dt, inter, k = torch.bfloat16, 1792, 8192
+    x = torch.randn(m, k, dtype=dt, device="cuda")
+    wq, s, deq = _fp8(torch.randn(2 * inter, k, dtype=dt, device="cuda") * 0.02, "silu")
+    g = _norm_ref(x).float() @ deq.t()
+    o32 = torch.nn.functional.silu(g[:, :inter]) * g[:, inter:]
+    ops.set_wide_plan(*plan)
+    got = ops.decode_gate_up_silu(x, wq, 1e-5, w_scale=s)
+    close(got, o32, 6e-2, 4e-2)
+
+
+def test_wide_fp8_matches_skinny_at_the_seam():
+    """fp8: 32 rows (16-row-tile W8 GEMV) and 33 rows (wide W8 build) agree on the first 32."""
+    torch.manual_seed(49)
+    dt = torch.bfloat16
+    x = torch.randn(33, 4096, dtype=dt, device="cuda")
+    wq, s, _ = _fp8(torch.randn(4096, 4096, dtype=dt, device="cuda") * 0.02)
+    a = ops.linear(x[:32].contiguous(), wq, w_scale=s)
+    b = ops.linear(x, wq, w_scale=s)
+    close(b[:32], a, 2e-2, 1e-2)
