@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import json
 import math
+import os
 from dataclasses import dataclass
 from pathlib import Path
 
@@ -333,7 +334,10 @@ class LlamaModel:
         # attention: 5 launches per layer at weight-stream speed instead of ~9 with the
         # row-major skinny / library GEMMs (17 rows: 168 -> ~80 us of GEMMs per layer,
         # profiles/r4_small_prefill_fused.txt)
-        small = self.small_prefill_ok(T)
+        # fp8 steps of 129.. rows in the MIDM_FP8_ROWS range run every projection on the
+        # mid-M kernel's W8 builds (all or nothing: the library fp8 chain defers each down
+        # product into the next layer's norm-quant kernel, which a fused qkv cannot take)
+        small = self.small_prefill_ok(T) or (fp8 and self.midm_fp8_ok(T))
         # 129..640-row steps (uncached burst / planning prefills): per projection, the mid-M
         # kernel (ops/csrc/midm.h, fused epilogues) where it beats the tuned library GEMM +
         # separate norm / RoPE / SiLU kernels, the library elsewhere (midm_route)
@@ -384,7 +388,12 @@ class LlamaModel:
                 self._row_parallel(attn.view(T, nq * D), L, "o", residual)
             else:
                 self._proj_residual(attn.view(T, nq * D), L.o, L.o_s, residual, "o")
-            if small or mid.get("gate_up"):
+            if small and fp8 and T > self._fp8_gate_up_max():
+                # fp8 gate_up past its crossover: the library fp8 GEMM on row-quantised
+                # activations (norm fused into the quantiser), bf16 SiLU-mul for the fused down
+                xq, xs = ops.quant_rows_fp8(residual, ops.QUANT_NORM, L.post_norm, eps)
+                a = ops.silu_and_mul(self._gemm8(xq, xs, L.gate_up, L.gate_up_s, dt, "gate_up"))
+            elif small or mid.get("gate_up"):
                 a = ops.decode_gate_up_silu(residual, L.gate_up_ps if ps else L.gate_up, eps,
                                             preshuffled=ps, w_scale=L.gate_up_s)
             else:
@@ -498,6 +507,43 @@ class LlamaModel:
             return {}
         return {p: any(lo <= T <= hi for lo, hi in r) for p, r in self.MIDM_ROUTES.items()}
 
+    # fp8 (weight-only) steps of these rows run the whole layer on the mid-M kernel's W8
+    # builds instead of the row-quantised library fp8 GEMMs (ATTA_MIDM_FP8_ROWS="lo-hi").  Off
+    # by default: the library's fp8 MFMA GEMMs win from 274 rows on at the 8B shapes (bench
+    # fp8 uncached planning 274 rows 5.68 vs 7.47 ms, burst 392 rows 6.42 vs 9.35 ms,
+    # profiles/r6_midm_fp8_negative.txt) - the W8 builds run bf16 MFMAs at ~35 % busy
+    _fp8_rows = os.environ.get("ATTA_MIDM_FP8_ROWS", "0")
+    MIDM_FP8_ROWS = ((0, -1) if _fp8_rows in ("", "0") else
+                     tuple(int(v) for v in _fp8_rows.split("-")))
+
+    # fp8 weights, TP = 1: most rows of a fused-path step whose gate_up + SiLU still runs the
+    # wide kernel's W8 build, by hidden size; past it the library fp8 GEMM wins (cold weights,
+    # bench_wide --fp8 --tuned, profiles/r6_wide_fp8.txt: 8B 38.4 vs 47.4 us at 75 rows, 50.9
+    # vs 47.4 at 128; 70B 106 vs 117 at 33 rows, 123 vs 118 at 64).  qkv / o / down keep the
+    # W8 builds to 128 rows (1.14-1.9x at <= 96 rows, 0.93-0.97x at 128 on the 70B shapes)
+    FP8_GATE_UP_WIDE_MAX = {4096: 112, 8192: 48}
+    # and the whole fused step: 70B fp8 prefill 33 / 76 / 128 rows 15.4 / 21.4 / 24.3 ms fused
+    # vs 20.6 / 22.4 / 23.3 on the library chain (profiles/r6_70b_fp8_planning_prefill.txt)
+    FP8_FUSED_MAX_ROWS = {8192: 112}
+
+    def _fp8_fused_max(self) -> int:
+        if self.tp_size > 1:
+            return 128
+        return self.FP8_FUSED_MAX_ROWS.get(self.cfg.hidden_size, 128)
+
+    def _fp8_gate_up_max(self) -> int:
+        if self.tp_size > 1:
+            return 128  # the TP shards' library GEMMs are launch-bound: not measured past it
+        return self.FP8_GATE_UP_WIDE_MAX.get(self.cfg.hidden_size, 128)
+
+    def midm_fp8_ok(self, T: int) -> bool:
+        """Does an fp8 step of T > 128 rows run every projection on the mid-M W8 builds?"""
+        lo, hi = self.MIDM_FP8_ROWS
+        return (self.quant == "fp8" and 128 < T and lo <= T <= hi
+                and T <= ops.fused_max_rows(True, True) and self.tp_size == 1
+                and self.fused_decode and self.small_prefill_fused
+                and self.device.type == "cuda" and self.decode_fusable(T))
+
     def small_prefill_ok(self, T: int) -> bool:
         """Does a (prefill or mixed) step of T rows run on the fused decode kernels - RMSNorm
         folded into the pre-shuffled skinny GEMVs, RoPE + KV write in the QKV epilogue, SiLU-mul
@@ -506,10 +552,11 @@ class LlamaModel:
         turns the fused kernels off here too).  Up to 128 rows, 16-bit or fp8 weights, any TP
         degree (the row-parallel sums go through _row_parallel); past 128 rows every
         projection is routed on its own (midm_route)."""
+        if self.quant == "fp8":
+            if T > self._fp8_fused_max() or not (self.layers and self.layers[0].qkv_ps is not None):
+                return False
         return (self.small_prefill_fused and self.fused_decode and self.device.type == "cuda"
-                and T <= 128 and self.decode_fusable(T)
-                and (self.quant != "fp8" or (bool(self.layers)
-                                             and self.layers[0].qkv_ps is not None)))
+                and T <= 128 and self.decode_fusable(T))
 
     def decode_fusable(self, num_tokens: int) -> bool:
         """Can a step of this many rows run the fused weight-streaming kernels?  <= 32 rows:

@@ -341,12 +341,10 @@ MIDM_MAX_M = int(os.environ.get("ATTA_MIDM_MAX_M", "1024"))
 def fused_max_rows(preshuffled: bool = True, fp8: bool = False) -> int:
     """Most rows a call may have to run on the hand-written weight-streaming kernels (the
     16-row-tile GEMVs, the wide small-M kernel, the mid-M kernel) for this weight format:
-    pre-shuffled fp8 weights run the wide kernel's W8 builds up to 128 rows (the mid-M kernel
-    is 16-bit only)."""
+    pre-shuffled 16-bit or fp8 weights (the W8 builds of the wide / mid-M kernels)."""
+    del fp8  # both kernels have fp8-weight builds
     if not preshuffled or WIDE_MAX_M <= SKINNY_MAX_M:
         return SKINNY_MAX_M
-    if fp8:
-        return min(WIDE_MAX_M, 128)
     if WIDE_MAX_M >= 128 and MIDM_MAX_M > 128:
         return MIDM_MAX_M
     return min(WIDE_MAX_M, 128)

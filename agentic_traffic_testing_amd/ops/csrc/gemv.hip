@@ -219,10 +219,11 @@ void atta_get_wide_min_rows(int* m, int* m_silu) {
 }
 // pre-shuffled 16-bit calls of up to this many rows run the wide (<= 128) or mid-M kernels
 constexpr int kMidmMaxM = 8192;
-// rows one call may carry: row-major weights the 16-row-tile GEMV (<= 32); pre-shuffled fp8
-// weights also the wide kernel's W8 builds (<= 128); pre-shuffled 16-bit the mid-M kernel too
+// rows one call may carry: row-major weights the 16-row-tile GEMV (<= 32); pre-shuffled
+// 16-bit or fp8 weights also the wide (<= 128) and mid-M kernels
 static int max_rows(int ps, const float* wscale) {
-  return !ps ? 32 : (wscale != nullptr ? 128 : kMidmMaxM);
+  (void)wscale;
+  return !ps ? 32 : kMidmMaxM;
 }
 static bool use_wide(int M, int ps, const float* wscale, bool silu = false) {
   return M > 32 ||
@@ -258,9 +259,7 @@ static int wide(SkinnyParams& p, int epi, int ntiles, int dtype, hipStream_t str
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -2;
   const SplitKWs& w = g_splitk[dev];
   if (p.M > 128) {
-    // past the wide kernel's 8 row blocks: the mid-M kernel (midm.hip, row-blocked grid;
-    // 16-bit weights only)
-    if (p.wscale != nullptr) return -1;
+    // past the wide kernel's 8 row blocks: the mid-M kernel (midm.hip, row-blocked grid)
     p.wg_trace = nullptr;
     return atta_midm_launch(p, epi, ntiles, dtype, w.ws, w.ws_floats, stream);
   }

@@ -53,7 +53,11 @@ struct Geo {
   int R;            // rows of the split-K slab layout (M padded to 16)
 };
 
-template <typename T, int BMT, int EPI, bool NORM, int XD>
+// W8: fp8 (e4m3fn) weights in the 16-row x 64-K blocks of the skinny GEMV (skinny.h) - a
+// wave's two K steps of a chunk (2 kg, 2 kg + 1) are exactly one such block, one 16-B load
+// per tile per chunk - converted to 16-bit MFMA operands in registers, the per-row scale on
+// the finished accumulators (weight-only quantisation, as wide.h)
+template <typename T, int BMT, int EPI, bool NORM, int XD, bool W8 = false>
 __global__ __launch_bounds__(kThr) void midm_kernel(SkinnyParams p, Geo g) {
   using MF = MfmaK32<T>;
   using frag8 = typename MF::frag8;
@@ -68,7 +72,8 @@ __global__ __launch_bounds__(kThr) void midm_kernel(SkinnyParams p, Geo g) {
   // two x sets / buffers (three buffers of 192 rows cost them their LDS headroom)
   constexpr int NXB = XD == 1 ? 3 : 2;
   constexpr int LDSB = NXB * XBUF > REDB ? NXB * XBUF : REDB;
-  constexpr int NWF = kNTW * 2;  // weight fragments per chunk per wave (2 K steps x tiles)
+  constexpr int NW = W8 ? 1 : 2;  // 16-B weight loads per tile per chunk
+  constexpr int NWF = kNTW * NW;  // weight registers (u32x4) per chunk per wave
   constexpr int RPL = (BM + 63) / 64;
   constexpr int kWStages = XD == 1 ? 3 : wstages(BMT);
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDSB];
@@ -93,12 +98,14 @@ __global__ __launch_bounds__(kThr) void midm_kernel(SkinnyParams p, Geo g) {
   const int nch = p.K / kKC;
   const int c0 = ks * nch / g.S, c1 = (ks + 1) * nch / g.S;
 
-  // weight fragment base of tile j, K step (c, s): wp[j] + (4 c + 2 kg + s) * 512 elements
-  const uint16_t* wp[kNTW];
+  // weight bytes of tile j: 16-bit, K step (c, s) at wp[j] + (4 c + s) * 1 KiB (this wave's
+  // steps 2 kg + s); fp8, chunk c at wp[j] + 2 c * 1 KiB (the block of steps 2 kg, 2 kg + 1)
+  const unsigned char* wp[kNTW];
 #pragma unroll
   for (int j = 0; j < kNTW; ++j)
-    wp[j] = p.w + static_cast<int64_t>(tile0 + j < g.ntiles ? tile0 + j : 0) * (p.K / 32) * 512 +
-            2 * kg * 512 + lane * 8;
+    wp[j] = reinterpret_cast<const unsigned char*>(p.w) +
+            static_cast<int64_t>(tile0 + j < g.ntiles ? tile0 + j : 0) * (p.K / (W8 ? 64 : 32)) * 1024 +
+            (W8 ? kg : 2 * kg) * 1024 + lane * 16;
   // x pieces of this thread: piece q = tid + i * kThr -> staged row q / 16, slot q % 16
   int xsrc[PPT];
   int xdst[PPT];
@@ -129,8 +136,15 @@ __global__ __launch_bounds__(kThr) void midm_kernel(SkinnyParams p, Geo g) {
 #pragma unroll
     for (int j = 0; j < kNTW; ++j)
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
-        f[j * 2 + s] = *reinterpret_cast<const u32x4*>(wp[j] + (c * 4 + s) * 512);
+      for (int s = 0; s < NW; ++s)
+        f[j * NW + s] = *reinterpret_cast<const u32x4*>(wp[j] + (c * (W8 ? 2 : 4) + s) * 1024);
+  };
+  // MFMA B operand of tile j, K step s (fp8: converted here, ahead of the MFMA groups)
+  auto wfrag = [&](const u32x4 (&f)[NWF], int j, int s) -> frag8 {
+    if constexpr (W8)
+      return s ? fp8x8_to_frag<T>(f[j][2], f[j][3]) : fp8x8_to_frag<T>(f[j][0], f[j][1]);
+    else
+      return __builtin_bit_cast(frag8, f[j * 2 + s]);
   };
   auto load_x = [&](u32x4 (&xr)[PPT], int c) {
 #pragma unroll
@@ -157,6 +171,11 @@ __global__ __launch_bounds__(kThr) void midm_kernel(SkinnyParams p, Geo g) {
   // waves idle on LDS latency between MFMA pairs (one barrier per chunk, two waves per SIMD)
   auto compute = [&](const u32x4 (&f)[NWF], int buf) {
     const unsigned char* bb = lds + buf * XBUF + col * kRowB;
+    frag8 wf[kNTW][2];
+#pragma unroll
+    for (int j = 0; j < kNTW; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) wf[j][s] = wfrag(f, j, s);
     if constexpr (BMT <= 8) {
       frag8 xf[2][BMT];
 #pragma unroll
@@ -172,7 +191,7 @@ __global__ __launch_bounds__(kThr) void midm_kernel(SkinnyParams p, Geo g) {
         for (int t = 0; t < BMT; ++t)
 #pragma unroll
           for (int j = 0; j < kNTW; ++j)
-            acc[j][t] = MF::mma(xf[s][t], __builtin_bit_cast(frag8, f[j * 2 + s]), acc[j][t]);
+            acc[j][t] = MF::mma(xf[s][t], wf[j][s], acc[j][t]);
       // pin the order (hipcc otherwise sinks each read next to its MFMA pair): all reads,
       // then the MFMAs, with counted lgkmcnt waits between them
       __builtin_amdgcn_sched_group_barrier(0x100, 2 * BMT, 0);          // DS read
@@ -186,7 +205,7 @@ __global__ __launch_bounds__(kThr) void midm_kernel(SkinnyParams p, Geo g) {
           const frag8 xf = *reinterpret_cast<const frag8*>(bb + t * 16 * kRowB + off);
 #pragma unroll
           for (int j = 0; j < kNTW; ++j)
-            acc[j][t] = MF::mma(xf, __builtin_bit_cast(frag8, f[j * 2 + s]), acc[j][t]);
+            acc[j][t] = MF::mma(xf, wf[j][s], acc[j][t]);
         }
       }
     }
@@ -296,6 +315,17 @@ __global__ __launch_bounds__(kThr) void midm_kernel(SkinnyParams p, Geo g) {
     }
   }
 
+  if constexpr (W8) {
+    // dequant: lane column col of tile j is weight row tile_row(tile, col)
+#pragma unroll
+    for (int j = 0; j < kNTW; ++j) {
+      const float sc = p.wscale[tile_row<EPI>(tile0 + j < g.ntiles ? tile0 + j : 0, col, p)];
+#pragma unroll
+      for (int t = 0; t < BMT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[j][t][i] *= sc;
+    }
+  }
   // ---- row sums of squares (the 16 lanes staging one row are consecutive) ---------------
   if constexpr (NORM) {
 #pragma unroll
@@ -370,8 +400,8 @@ __global__ __launch_bounds__(kThr) void midm_kernel(SkinnyParams p, Geo g) {
 constexpr bool norm_fits(int bmt) { return bmt <= 8; }
 
 // launch one (BMT) instantiation; -1 = epilogue / norm combination not built
-template <typename T, int BMT, int XD>
-inline int launch_bmt(int epi, dim3 grid, hipStream_t st, const SkinnyParams& p, const Geo& g) {
+template <typename T, int BMT, int XD, bool W8>
+inline int launch_bmt_w(int epi, dim3 grid, hipStream_t st, const SkinnyParams& p, const Geo& g) {
   const dim3 blk(kThr);
   const bool norm = p.eps > 0.f;
   if constexpr (!norm_fits(BMT)) {
@@ -380,22 +410,28 @@ inline int launch_bmt(int epi, dim3 grid, hipStream_t st, const SkinnyParams& p,
   switch (epi) {
     case EPI_PLAIN:
       if (norm) return -1;
-      midm_kernel<T, BMT, EPI_PLAIN, false, XD><<<grid, blk, 0, st>>>(p, g);
+      midm_kernel<T, BMT, EPI_PLAIN, false, XD, W8><<<grid, blk, 0, st>>>(p, g);
       return 0;
     case EPI_RESADD:
       if (norm) return -1;
-      midm_kernel<T, BMT, EPI_RESADD, false, XD><<<grid, blk, 0, st>>>(p, g);
+      midm_kernel<T, BMT, EPI_RESADD, false, XD, W8><<<grid, blk, 0, st>>>(p, g);
       return 0;
     case EPI_QKVROPE:
       if (!norm || g.S > 1) return -1;
-      if constexpr (norm_fits(BMT)) midm_kernel<T, BMT, EPI_QKVROPE, true, XD><<<grid, blk, 0, st>>>(p, g);
+      if constexpr (norm_fits(BMT)) midm_kernel<T, BMT, EPI_QKVROPE, true, XD, W8><<<grid, blk, 0, st>>>(p, g);
       return 0;
     case EPI_SILU:
       if (!norm || g.S > 1) return -1;
-      if constexpr (norm_fits(BMT)) midm_kernel<T, BMT, EPI_SILU, true, XD><<<grid, blk, 0, st>>>(p, g);
+      if constexpr (norm_fits(BMT)) midm_kernel<T, BMT, EPI_SILU, true, XD, W8><<<grid, blk, 0, st>>>(p, g);
       return 0;
     default: return -1;
   }
+}
+
+template <typename T, int BMT, int XD>
+inline int launch_bmt(int epi, dim3 grid, hipStream_t st, const SkinnyParams& p, const Geo& g) {
+  return p.wscale != nullptr ? launch_bmt_w<T, BMT, XD, true>(epi, grid, st, p, g)
+                             : launch_bmt_w<T, BMT, XD, false>(epi, grid, st, p, g);
 }
 
 // per-BMT translation units (midm_b<N>.hip), built in parallel

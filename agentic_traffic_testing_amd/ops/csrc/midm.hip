@@ -90,7 +90,7 @@ struct Cost {
   double mfma_eff = 0.35, cu_bps = 52e3, ramp = 2.0, red_fixed = 6.0, red_bps = 1.5e6;
 };
 
-static double plan_cost(const Cost& c, int M, int ntiles, int K, int bmt, int S) {
+static double plan_cost(const Cost& c, int M, int ntiles, int K, int bmt, int S, bool w8) {
   const int bm = 16 * bmt;
   const int nrb = (M + bm - 1) / bm;
   const int ncb = (ntiles + kTPB - 1) / kTPB;
@@ -98,7 +98,7 @@ static double plan_cost(const Cost& c, int M, int ntiles, int K, int bmt, int S)
   const double rounds = std::ceil(wgs / 256.0);
   const double ks = static_cast<double>(K) / S;
   const double t_mfma = bm * 128.0 * ks / (2048.0 * c.mfma_eff) / 2400.0;
-  const double t_load = (bm + 128.0) * ks * 2.0 / c.cu_bps;
+  const double t_load = (bm * 2.0 + 128.0 * (w8 ? 1.0 : 2.0)) * ks / c.cu_bps;
   double t = rounds * ((t_mfma > t_load ? t_mfma : t_load) + c.ramp);
   if (S > 1) {
     const int R = (M + 15) / 16 * 16;
@@ -107,8 +107,8 @@ static double plan_cost(const Cost& c, int M, int ntiles, int K, int bmt, int S)
   return t;
 }
 
-static void plan(int M, int ntiles, int K, bool can_split, bool norm, int64_t ws_floats,
-                 int& bmt, int& S) {
+static void plan(int M, int ntiles, int K, bool can_split, bool norm, bool w8,
+                 int64_t ws_floats, int& bmt, int& S) {
   static const Cost c;
   const int nch = K / kKC;
   const int R = (M + 15) / 16 * 16;
@@ -120,7 +120,7 @@ static void plan(int M, int ntiles, int K, bool can_split, bool norm, int64_t ws
     for (int s = 1; s <= (can_split ? 8 : 1); ++s) {
       if (nch / s < 2) break;
       if (s > 1 && static_cast<int64_t>(ntiles) * s * R * 16 > ws_floats) break;
-      const double t = plan_cost(c, M, ntiles, K, b, s);
+      const double t = plan_cost(c, M, ntiles, K, b, s, w8);
       if (t < best - 1e-9) {
         best = t;
         bmt = b;
@@ -145,22 +145,23 @@ void atta_set_midm_plan(int bmt, int ksplit) {
 
 int atta_midm_plan(int M, int ntiles, int K, int epi, int64_t ws_floats, int* bmt, int* ksplit) {
   const bool can_split = epi == EPI_PLAIN || epi == EPI_RESADD;
-  midm::plan(M, ntiles, K, can_split, !can_split, ws_floats, *bmt, *ksplit);
+  midm::plan(M, ntiles, K, can_split, !can_split, false, ws_floats, *bmt, *ksplit);
   return 0;
 }
 
 // Launch the mid-M kernel for a SkinnyParams filled by a gemv.hip entry point (x, w
-// pre-shuffled 16-bit, y / epilogue fields, eps, M, N, K).  ntiles: 16-column weight tiles
+// pre-shuffled 16-bit or fp8 with p.wscale, y / epilogue fields, eps, M, N, K).  ntiles: 16-column weight tiles
 // (SiLU: inter / 8).  Returns 0, -1 (unsupported shape / plan) or -2 (split-K workspace).
 int atta_midm_launch(SkinnyParams& p, int epi, int ntiles, int dtype, float* sk_ws,
                      int64_t ws_floats, hipStream_t stream) {
-  if (p.M < 1 || p.K % midm::kKC != 0 || !p.ps || p.wscale != nullptr) return -1;
+  if (p.M < 1 || p.K % midm::kKC != 0 || !p.ps) return -1;
   if (epi != EPI_PLAIN && epi != EPI_RESADD && epi != EPI_QKVROPE && epi != EPI_SILU) return -1;
   const bool can_split = epi == EPI_PLAIN || epi == EPI_RESADD;
   int bmt = g_midm_bmt, S = g_midm_ksplit;
   g_midm_bmt = g_midm_ksplit = 0;
   if (bmt <= 0 || S <= 0)
-    midm::plan(p.M, ntiles, p.K, can_split, p.eps > 0.f, sk_ws ? ws_floats : 0, bmt, S);
+    midm::plan(p.M, ntiles, p.K, can_split, p.eps > 0.f, p.wscale != nullptr,
+               sk_ws ? ws_floats : 0, bmt, S);
   if (S > 1 && !can_split) return -1;
   if (S < 1 || p.K / midm::kKC < S) return -1;
   // a split whose slabs do not fit the workspace is halved until they do (forced plans)

@@ -582,17 +582,38 @@ inline int launch_epi_w8(int epi, dim3 grid, hipStream_t st, const SkinnyParams&
   }
 }
 
+// (the non-norm fp8 epilogues of the builds whose norm fold spills)
+template <typename T, int WAVES, int MT, int TPW>
+inline int launch_epi_w8_plain(int epi, dim3 grid, hipStream_t st, const SkinnyParams& p,
+                               int ntiles) {
+  const dim3 blk(WAVES * 64);
+  if (p.eps > 0.f) return -1;
+  switch (epi) {
+    case EPI_PLAIN:
+      wide_kernel<T, WAVES, MT, EPI_PLAIN, false, TPW, true><<<grid, blk, 0, st>>>(p, ntiles);
+      return 0;
+    case EPI_RESADD:
+      wide_kernel<T, WAVES, MT, EPI_RESADD, false, TPW, true><<<grid, blk, 0, st>>>(p, ntiles);
+      return 0;
+    default: return -1;
+  }
+}
+
 template <typename T, int WAVES, int MT, int TPW>
 inline int launch_epi(int epi, dim3 grid, hipStream_t st, const SkinnyParams& p, int ntiles) {
   const dim3 blk(WAVES * 64);
   const bool norm = p.eps > 0.f;
+  constexpr bool kNormOk = norm_fits(WAVES, MT, TPW);
   if (p.wscale != nullptr) {
-    // fp8 weights: built for 4 and 8 waves (the plan offers only those)
-    if constexpr ((WAVES == 4 || WAVES == 8) && TPW == 1)
-      return launch_epi_w8<T, WAVES, MT, TPW>(epi, grid, st, p, ntiles);
+    // fp8 weights (every wave count: 7 waves tile the 70B gate_up's 3584 SiLU tiles into
+    // exactly two rounds of 256 workgroups)
+    if constexpr (TPW == 1) {
+      if (norm && !kNormOk) return -1;
+      if constexpr (kNormOk) return launch_epi_w8<T, WAVES, MT, TPW>(epi, grid, st, p, ntiles);
+      return launch_epi_w8_plain<T, WAVES, MT, TPW>(epi, grid, st, p, ntiles);
+    }
     return -1;
   }
-  constexpr bool kNormOk = norm_fits(WAVES, MT, TPW);
   if constexpr (!kNormOk) {
     if (norm) return -1;
   }

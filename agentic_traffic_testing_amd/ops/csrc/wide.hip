@@ -142,7 +142,6 @@ static void plan(int ntiles, int K, int M, bool norm, bool w8, int& waves, int& 
     for (int wi = 0; wi < 4; ++wi) {
       const int w = ws[wi];
       if (norm && !norm_fits(w, (M + 15) / 16, tp)) continue;  // see launch_epi
-      if (w8 && w != 4 && w != 8) continue;                     // fp8 builds (launch_epi)
       if (tp == 2 && !tpw2_built(w)) continue;
       const int tb = w * tp;
       const int ncb = (ntiles + tb - 1) / tb;
@@ -181,7 +180,7 @@ int atta_wide_launch(SkinnyParams& p, int epi, int ntiles, int waves, int ksplit
                      const float* sk_ws, int* sk_counters, int64_t ws_floats, int n_counters,
                      hipStream_t stream) {
   if (p.M < 1 || p.M > 128 || p.K % wide::kKC != 0 || !p.ps) return -1;
-  const bool w8 = p.wscale != nullptr;  // fp8 weights (W8 builds: 4 / 8 waves)
+  const bool w8 = p.wscale != nullptr;  // fp8 weights (the W8 builds)
   // waves 14 / 16 / 17 / 18 in an explicit plan = 4 / 6 / 7 / 8 waves x two tiles per wave
   // (measured slower and not built: such a plan returns -1 from the launcher)
   int tpw = 1;

@@ -18,6 +18,9 @@ from agentic_traffic_testing_amd import ops  # noqa: E402
 from agentic_traffic_testing_amd.ops import reference as ref  # noqa: E402
 
 SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+# Llama-3-70B TP=1 (--model 70b): 64 q / 8 kv heads, hidden 8192, FFN 28672
+SHAPES_70B = {"qkv": (10240, 8192), "o": (8192, 8192), "gate_up": (57344, 8192),
+              "down": (8192, 28672)}
 PLANS = {"qkv": [(6, 4), (8, 4), (6, 2), (4, 4), (8, 6)],
          "o": [(8, 8), (4, 4), (8, 4), (4, 8), (6, 6)],
          "gate_up": [(7, 1), (8, 1), (4, 1), (4, 2), (8, 2)],
@@ -77,6 +80,10 @@ def main():
     ap.add_argument("--tuned", action="store_true",
                     help="library arm on the shipped tuned table, rows padded to its buckets "
                          "(as the engine runs it)")
+    ap.add_argument("--model", choices=["8b", "70b"], default="8b")
+    ap.add_argument("--fp8", action="store_true",
+                    help="fp8 weights: the W8 builds vs the engine's library fp8 chain "
+                         "(row-quantised activations + hipBLASLt fp8 GEMM)")
     a = ap.parse_args()
     global GRAPH
     GRAPH = a.graph
@@ -84,21 +91,30 @@ def main():
     ops.ensure_splitk_workspace("cuda")
     if a.tuned:
         from agentic_traffic_testing_amd import tuning
-        print("tuned table:", tuning.load("auto", "llama-3.1-8b"), flush=True)
+        print("tuned table:", tuning.load("auto", "llama-3.1-8b" if a.model == "8b"
+                                          else "llama-3-70b"), flush=True)
     dt = torch.bfloat16
-    hq, hkv, bs, nb = 32, 8, 16, 512
+    hq, hkv, bs, nb = (32 if a.model == "8b" else 64), 8, 16, 512
+    shapes = SHAPES if a.model == "8b" else SHAPES_70B
     kc = torch.zeros(nb, hkv, bs, 128, dtype=dt, device="cuda")
     vc = torch.zeros(nb, hkv, 128, bs, dtype=dt, device="cuda")
     cs = ref.rope_cos_sin(128, 8192, 500000.0, None, device="cuda")
-    ones = torch.ones(4096, dtype=dt, device="cuda")
+    ones = torch.ones(8192, dtype=dt, device="cuda")
     tot = {}
     for proj in a.proj:
-        n, k = SHAPES[proj]
-        mb = n * k * 2 / 1e6
+        n, k = shapes[proj]
+        mb = n * k * (1 if a.fp8 else 2) / 1e6
         ncopy = max(2, int(600 // mb) + 1)
         rowmap = {"qkv": "qkv", "gate_up": "silu"}.get(proj, "plain")
         raw = [(torch.randn(n, k, device="cuda") * 0.02).to(dt) for _ in range(ncopy)]
-        wps = [ops.preshuffle(w, rowmap) for w in raw]
+        scales = [None] * ncopy
+        if a.fp8:
+            qs = [ops.quantize_fp8(w) for w in raw]
+            raw = [q for q, _ in qs]
+            scales = [sc for _, sc in qs]
+            wps = [ops.preshuffle_fp8(q, rowmap) for q in raw]
+        else:
+            wps = [ops.preshuffle(w, rowmap) for w in raw]
         for m in a.m:
             x = torch.randn(m, k, device="cuda").to(dt)
             res = torch.zeros(m, n, dtype=dt, device="cuda")
@@ -110,15 +126,15 @@ def main():
             def wide(i, plan=(0, 0), mplan=(0, 0)):
                 ops.set_wide_plan(*plan)
                 ops.set_midm_plan(*mplan)
-                w = wps[i % ncopy]
+                w, sc = wps[i % ncopy], scales[i % ncopy]
                 if proj == "qkv":
                     ops.decode_qkv_rope(x, w, 1e-5, pos, slots, cs, kc, vc, hq, hkv, q_out=q,
-                                        preshuffled=True)
+                                        preshuffled=True, w_scale=sc)
                 elif proj == "gate_up":
-                    ops.decode_gate_up_silu(x, w, 1e-5, out=act, preshuffled=True)
+                    ops.decode_gate_up_silu(x, w, 1e-5, out=act, preshuffled=True, w_scale=sc)
                 else:  # as models/llama.py forward_decode calls it
                     ops.linear(x, w, residual=res, preshuffled=True, ksplit=None, proj=proj,
-                               waves=ops.decode_waves(proj, True, False))
+                               waves=ops.decode_waves(proj, True, a.fp8), w_scale=sc)
 
             ml = m
             if a.tuned and m > 32:
@@ -130,11 +146,24 @@ def main():
 
             def lib(i):
                 w = raw[i % ncopy]
+                if a.fp8:  # models/llama.py forward's fp8 chain
+                    sc = scales[i % ncopy]
+                    if proj == "qkv":
+                        xq, xs = ops.quant_rows_fp8(xl, ops.QUANT_NORM, ones[:k], 1e-5)
+                        y = ops.gemm_fp8(xq, xs, w, sc, dt)
+                        ops.rope_cache(y, posl, posl, cs, kc, vc, hq, hkv, 128)
+                    elif proj == "gate_up":
+                        xq, xs = ops.quant_rows_fp8(xl, ops.QUANT_NORM, ones[:k], 1e-5)
+                        ops.quant_rows_fp8(ops.gemm_fp8(xq, xs, w, sc, dt), ops.QUANT_SILU)
+                    else:
+                        xq, xs = ops.quant_rows_fp8(xl)
+                        ops.gemm_fp8(xq, xs, w, sc, dt)
+                    return
                 if proj == "qkv":
-                    y = torch.nn.functional.linear(ops.rms_norm(xl, ones, 1e-5), w)
+                    y = torch.nn.functional.linear(ops.rms_norm(xl, ones[:k], 1e-5), w)
                     ops.rope_cache(y, posl, posl, cs, kc, vc, hq, hkv, 128)
                 elif proj == "gate_up":
-                    ops.silu_and_mul(torch.nn.functional.linear(ops.rms_norm(xl, ones, 1e-5), w))
+                    ops.silu_and_mul(torch.nn.functional.linear(ops.rms_norm(xl, ones[:k], 1e-5), w))
                 else:
                     resl.addmm_(xl, w.t())
 

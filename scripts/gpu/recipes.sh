@@ -18,6 +18,17 @@
 #   burst        windowed profile of the 380-row burst prefill (r4_prof_burst380_summary.txt)
 #   small        17 / 85-row prefill profiles and the cached-regime bench with the fused small-prefill
 #                path on / off (r4_small_prefill_fused.txt)
+# Rounds 5-6:
+#   wide         wide small-M GEMM vs the library, graph replay, 33-128 rows (r5_wide_gemm.txt,
+#                r6_wide_gemm_sched.txt)
+#   midm         mid-M GEMM vs the tuned library and its (row block, split) sweep, 129-640 rows
+#                (r6_midm_vs_tuned.txt, r6_midm_sweep.txt)
+#   fp8wide      fp8 weights: wide kernel W8 builds vs the library fp8 chain, 8B and 70B shapes
+#                (r6_wide_fp8.txt); fp8 mid-M route A/B on the bench (r6_midm_fp8_negative.txt)
+#   coldstart    first vs repeat TTFT of every fan-out step shape on a fresh engine
+#                (r6_coldstart_*.txt, tests/test_coldstart.py)
+#   fanout       per-episode TTFT by phase (r5_fanout_ttft_per_episode.txt)
+#   70bfp8       Llama-3-70B fp8 TP=1 bench, fused small-prefill path on / off (r6_70b_fp8.txt)
 set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 S=scripts/gpu/stages.sh
@@ -63,6 +74,34 @@ recipe() {
       TAG=r4sp85 STAGES=profpf TOKENS=85 SEQS=5 REPS=10 bash $S &&
       TAG=r4sf_on STAGES=bench STEPS=6 BENCH_ARGS="--warmup 5" bash $S &&
       TAG=r4sf_off STAGES=bench STEPS=6 BENCH_ARGS="--warmup 5 --set small_prefill_fused=0" bash $S ;;
+    wide)
+      timeout -k 10 400 python -u scripts/gpu/bench_wide.py --graph --m 33 48 64 75 80 96 112 128 \
+        > gpurun_out/wide_gemm.txt 2>&1 && tail -8 gpurun_out/wide_gemm.txt ;;
+    midm)
+      timeout -k 10 600 python -u scripts/gpu/bench_wide.py --tuned --m 129 188 256 382 475 640 \
+        > gpurun_out/midm_vs_tuned.txt 2>&1 &&
+      timeout -k 10 900 python -u scripts/gpu/bench_wide.py --tuned --midm-sweep --m 188 382 475 \
+        > gpurun_out/midm_sweep.txt 2>&1 && tail -4 gpurun_out/midm_vs_tuned.txt ;;
+    fp8wide)
+      timeout -k 10 500 python -u scripts/gpu/bench_wide.py --model 70b --fp8 --tuned --m 33 64 76 96 128 \
+        > gpurun_out/wide_70b_fp8.txt 2>&1 &&
+      timeout -k 10 300 python -u scripts/gpu/bench_wide.py --fp8 --tuned --m 33 75 128 \
+        > gpurun_out/wide_8b_fp8.txt 2>&1 &&
+      for v in 0 129-1024; do
+        ATTA_MIDM_FP8_ROWS=$v timeout -k 10 400 python -u bench.py --quantization fp8 --steps 2 \
+          --warmup 2 > gpurun_out/bench_8bfp8_midm_$v.log 2>&1 || return 1
+      done ;;
+    coldstart)
+      timeout -k 10 600 python -u -m agentic_traffic_testing_amd.bench.coldstart --reps 3 \
+        > gpurun_out/coldstart.txt 2>&1 && tail -1 gpurun_out/coldstart.txt ;;
+    fanout)
+      timeout -k 10 600 python -u scripts/gpu/probe_fanout_ttft.py --episodes 4 --warmup 5 \
+        > gpurun_out/fanout_ttft.txt 2>&1 && tail -12 gpurun_out/fanout_ttft.txt ;;
+    70bfp8)
+      for v in 1 0; do
+        timeout -k 10 560 python -u bench.py --model meta-llama/Llama-3-70B-Instruct --quantization fp8 \
+          --steps 1 --warmup 1 --set small_prefill_fused=$v > gpurun_out/bench_70bfp8_spf$v.log 2>&1 || return 1
+      done ;;
     *) echo "unknown recipe $1"; return 2 ;;
   esac
 }

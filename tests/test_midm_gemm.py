@@ -130,3 +130,54 @@ def test_midm_plan_fills_the_chip():
             assert wgs >= 160, (m, ntiles, k, bmt, s, wgs)
             if epi in (2, 3):
                 assert s == 1 and bmt <= 8
+
+
+# ---- fp8 weights (W8 builds: e4m3fn weight-only, per-row scales) ----------------------------
+def _fp8(w, rowmap="plain"):
+    q, s = ops.quantize_fp8(w)
+    deq = q.view(torch.float8_e4m3fn).float() * s[:, None]
+    return ops.preshuffle_fp8(q, rowmap), s, deq
+
+
+@pytest.mark.parametrize("plan", [(0, 0), (4, 1), (8, 2), (12, 1)])
+@pytest.mark.parametrize("m,n,k", [(129, 1024, 8192), (395, 8192, 8192), (640, 2048, 4096)])
+def test_midm_fp8_linear_plain_and_residual(plan, m, n, k):
+    torch.manual_seed(55)
+    dt = torch.bfloat16
+    x = torch.randn(m, k, dtype=dt, device="cuda")
+    wq, s, deq = _fp8(torch.randn(n, k, dtype=dt, device="cuda") * 0.02)
+    exp = x.float() @ deq.t()
+    assert ops.skinny_ok(x, wq, preshuffled=True, fp8=True)
+    ops.set_midm_plan(*plan)
+    got = ops.linear(x, wq, w_scale=s)
+    close(got, exp, 2e-2 * math.sqrt(k / 4096), 1e-2)
+    r = torch.randn(m, n, dtype=dt, device="cuda")
+    exp_r = exp.to(dt).float() + r.float()
+    ops.set_midm_plan(*plan)
+    ops.linear(x, wq, residual=r, w_scale=s)
+    close(r, exp_r, 3e-2 * math.sqrt(k / 4096), 1e-2)
+
+
+@pytest.mark.parametrize("m", [129, 395, 700])
+def test_midm_fp8_qkv_rope_and_gate_up(m):
+    torch.manual_seed(56)
+    dt, bs, nb, hq, hkv, H, inter = torch.bfloat16, 16, 128, 8, 1, 8192, 1792
+    x = torch.randn(m, H, dtype=dt, device="cuda") * 2
+    wq, s, deq = _fp8(torch.randn((hq + 2 * hkv) * 128, H, dtype=dt, device="cuda") * 0.02, "qkv")
+    pos = torch.randint(0, 4000, (m,), dtype=torch.int32, device="cuda")
+    slots = torch.randperm(nb * bs, device="cuda")[:m].to(torch.int32)
+    slots[1] = -1
+    cs = ref.rope_cos_sin(128, 8192, 500000.0, None, device="cuda")
+    k1 = torch.randn(nb, hkv, bs, 128, dtype=dt, device="cuda")
+    v1 = torch.randn(nb, hkv, 128, bs, dtype=dt, device="cuda")
+    k2, v2 = k1.clone(), v1.clone()
+    q_exp = ref.rope_cache(torch.nn.functional.linear(_norm_ref(x).float(), deq).to(dt), pos,
+                           slots, cs, k1, v1, hq, hkv, 128)
+    q_got = ops.decode_qkv_rope(x, wq, 1e-5, pos, slots, cs, k2, v2, hq, hkv, w_scale=s)
+    close(q_got, q_exp, 3e-2, 2e-2)
+    close(k2, k1, 3e-2, 2e-2)
+    close(v2, v1, 3e-2, 2e-2)
+    gq, gs, gdeq = _fp8(torch.randn(2 * inter, H, dtype=dt, device="cuda") * 0.02, "silu")
+    g = _norm_ref(x).float() @ gdeq.t()
+    o32 = torch.nn.functional.silu(g[:, :inter]) * g[:, inter:]
+    close(ops.decode_gate_up_silu(x, gq, 1e-5, w_scale=gs), o32, 6e-2, 4e-2)
