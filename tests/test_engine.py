@@ -523,8 +523,9 @@ def test_prefill_gemm_engine_matches_oracle(model):
 @pytest.mark.parametrize("model", ["small", "llama-8b-slice"])
 def test_prefill_splitk_route_engine_matches_oracle(model, monkeypatch):
     """prefill_gemm="auto" sends bf16 down_proj steps of 448-1152 rows to the split-K schedule
-    of the hand-written GEMM (models/llama.py _PG_SPLITK); a 600-token prompt prefilled in one
-    step must take that route and still match the fp32 dense oracle (near-tie rule), with the
+    of the hand-written GEMM (models/llama.py _PG_SPLITK) when no tuned table is loaded; a
+    700-token prompt prefilled in one step (past the mid-M kernel's down route, 129-640 rows)
+    must take that route and still match the fp32 dense oracle (near-tie rule), with the
     split-K wait never timing out (error word)."""
     from agentic_traffic_testing_amd import ops
     vocab = 30000 if model == "small" else 16000
@@ -540,7 +541,8 @@ def test_prefill_splitk_route_engine_matches_oracle(model, monkeypatch):
         return real(*args, **kw)
 
     monkeypatch.setattr(ops, "prefill_gemm", spy)
-    prompts = [list(np.random.default_rng(11).integers(300, vocab, size=600))]
+    prompts = [list(np.random.default_rng(11).integers(300, vocab, size=700))]
+    assert not eng.runner.model.midm_route(700).get("down")
     outs, bad = _check(eng, prompts, n=6, tol_logit=0.25)
     assert bad <= 1
     assert calls.count("splitk") == eng.runner.model.cfg.num_layers, calls
