@@ -7,45 +7,48 @@
 namespace atta {
 namespace midm {
 
-// Split-K combine + epilogue: one wave per (16-column tile, 16-row group); lane l loads columns
-// 4 (l >> 4) .. +3 of row (l & 15) from every slice (all issued together: one round trip for
-// S <= 8), sums them in slice order and lanes 0-15 run the unsplit path's epilogue on their row.
+// Split-K combine + epilogue: one wave per (16-column tile, 64-row group), one ROW per lane
+// (four 16-B loads per slice, up to 4 slices' loads in flight), summed in slice order -
+// bitwise deterministic - then the unsplit path's epilogue on the lane's row (wide.hip's
+// reduce, same layout).
 template <typename T, int EPI>
 __global__ __launch_bounds__(256) void midm_reduce_kernel(SkinnyParams p, int ntiles, int S, int R) {
-  __shared__ float red_all[4][16][17];
+  __shared__ float red_all[4][64][17];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int mt = R / 16;
+  const int nrg = (R + 63) / 64;
   const int gw = blockIdx.x * 4 + wid;
-  const int tile = gw / mt, rg = gw % mt;
+  const int tile = gw / nrg, rg = gw % nrg;
   if (tile >= ntiles) return;  // wave-uniform; no workgroup barrier below
-  const int r = rg * 16 + (lane & 15), qd = lane >> 4;
+  const int r = rg * 64 + lane;
   const int rc = min(r, max(p.M - 1, 0));
   wide::EpiIn<1> ein;
-  wide::epi_load<T, EPI, 1>(p, tile, rg * 16, 16, R, lane, ein);
-  f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < S; k0 += 8) {
-    f32x4 part[8];
+  wide::epi_load<T, EPI, 1>(p, tile, rg * 64, 64, R, lane, ein);
+  f32x4 sum[4] = {};
+  for (int k0 = 0; k0 < S; k0 += 4) {
+    f32x4 part[4][4];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 4; ++u) {
       const int s = min(k0 + u, S - 1);
-      part[u] = reinterpret_cast<const f32x4*>(
-          p.sk_ws + ((static_cast<int64_t>(tile) * S + s) * R + rc) * 16)[qd];
+      const f32x4* src =
+          reinterpret_cast<const f32x4*>(p.sk_ws + ((static_cast<int64_t>(tile) * S + s) * R + rc) * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) part[u][q] = src[q];
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) sum += (k0 + u < S) ? part[u] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sum[q] += (k0 + u < S) ? part[u][q] : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   float(*red)[17] = red_all[wid];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) red[lane & 15][4 * qd + e] = sum[e];
-  __builtin_amdgcn_wave_barrier();  // rows were written by 4 lanes each: in-wave hand-over
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  wide::epi_apply<T, EPI, 1>(p, tile, red, nullptr, rg * 16, false, ein);
+  for (int n = 0; n < 16; ++n) red[lane][n] = sum[n >> 2][n & 3];
+  wide::epi_apply<T, EPI, 1>(p, tile, red, nullptr, rg * 64, false, ein);
 }
 
 template <typename T>
 static int launch_reduce(int epi, const SkinnyParams& p, int ntiles, int S, int R,
                          hipStream_t st) {
-  const dim3 grid((ntiles * (R / 16) + 3) / 4), blk(256);
+  const dim3 grid((ntiles * ((R + 63) / 64) + 3) / 4), blk(256);
   switch (epi) {
     case EPI_PLAIN: midm_reduce_kernel<T, EPI_PLAIN><<<grid, blk, 0, st>>>(p, ntiles, S, R); return 0;
     case EPI_RESADD: midm_reduce_kernel<T, EPI_RESADD><<<grid, blk, 0, st>>>(p, ntiles, S, R); return 0;

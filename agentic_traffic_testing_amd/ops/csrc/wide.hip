@@ -7,61 +7,66 @@
 namespace atta {
 namespace wide {
 
-// Split-K combine + epilogue: one wave per (16-column tile, 16-row group); lane l loads
-// columns 4 (l >> 4) .. +3 of row (l & 15) from every slice (16 B each, all issued together:
-// one round trip for S <= 8), sums them in slice order - bitwise deterministic - with the row
-// sums of squares, and lanes 0-15 run the unsplit path's epi_apply on their row.  (One wave
-// per tile over all rows left most CUs idle: 10 us.)
+// Split-K combine + epilogue: one wave per (16-column tile, 64-row group), one ROW per lane -
+// lane l sums row 64 g + l's 16 columns over the slices (four 16-B loads per slice, the whole
+// row's slab reads of up to 4 slices in flight at once), sums of squares likewise, then runs
+// the unsplit path's epi_apply on its row with all 64 lanes.  (One wave per 16-row group, a
+// quarter row per lane and lanes 0-15 alone in the epilogue: 3x the waves, each with a quarter
+// of the loads in flight - 5.5 us per reduce at 85 rows, profiles/r5_burst_breakdown.txt.)
 template <typename T, int MT, int EPI, bool NORM>
 __global__ __launch_bounds__(256) void wide_reduce_kernel(SkinnyParams p, int ntiles, int S,
                                                          int tpb) {
   constexpr int R = MT * 16;
-  __shared__ float red_all[4][16][17];
-  __shared__ float inv_all[4][16];
+  constexpr int NRG = (R + 63) / 64;  // 64-row groups per tile
+  __shared__ float red_all[4][64][17];
+  __shared__ float inv_all[4][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int gw = blockIdx.x * 4 + wid;
-  const int tile = gw / MT, rg = gw % MT;
+  const int tile = gw / NRG, rg = gw % NRG;
   if (tile >= ntiles) return;  // wave-uniform; no workgroup barrier below
-  const int cb = tile / tpb;  // the main launch's column block (tiles per workgroup)
-  const int r = rg * 16 + (lane & 15), qd = lane >> 4;
-  const int rc = min(r, max(p.M - 1, 0));
+  const int cb = tile / tpb;   // the main launch's column block (tiles per workgroup)
+  const int r = rg * 64 + lane;
+  const int rc = min(r, min(R, max(p.M, 1)) - 1);
   EpiIn<1> ein;
-  epi_load<T, EPI, 1>(p, tile, rg * 16, 16, R, lane, ein);
-  f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+  epi_load<T, EPI, 1>(p, tile, rg * 64, 64, R, lane, ein);
+  f32x4 sum[4] = {};
   float ss = 0.f;
-  for (int k0 = 0; k0 < S; k0 += 8) {
-    f32x4 part[8];
-    float sp[8];
+  for (int k0 = 0; k0 < S; k0 += 4) {
+    f32x4 part[4][4];
+    float sp[4];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 4; ++u) {
       const int ks = min(k0 + u, S - 1);
-      part[u] = reinterpret_cast<const f32x4*>(
-          p.sk_ws + ((static_cast<int64_t>(tile) * S + ks) * R + rc) * 16)[qd];
+      const f32x4* src =
+          reinterpret_cast<const f32x4*>(p.sk_ws + ((static_cast<int64_t>(tile) * S + ks) * R + rc) * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) part[u][q] = src[q];
       if constexpr (NORM)
         sp[u] = p.sk_ws[static_cast<int64_t>(ntiles) * S * R * 16 +
                         (static_cast<int64_t>(cb) * S + ks) * R + rc];
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const bool real = k0 + u < S;
-      sum += real ? part[u] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < 4; ++u) {
+      const bool real = k0 + u < S;  // slice order: bitwise deterministic
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sum[q] += real ? part[u][q] : f32x4{0.f, 0.f, 0.f, 0.f};
       if constexpr (NORM) ss += real ? sp[u] : 0.f;
     }
   }
   float(*red)[17] = red_all[wid];
   float* inv_rms = inv_all[wid];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) red[lane & 15][4 * qd + e] = sum[e];
-  if (NORM && qd == 0) inv_rms[lane & 15] = rsqrtf(ss / static_cast<float>(p.K) + p.eps);
-  __builtin_amdgcn_wave_barrier();  // rows were written by 4 lanes each: in-wave hand-over
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  epi_apply<T, EPI, 1>(p, tile, red, inv_rms, rg * 16, NORM, ein);
+  for (int n = 0; n < 16; ++n) red[lane][n] = sum[n >> 2][n & 3];
+  if (NORM) inv_rms[lane] = rsqrtf(ss / static_cast<float>(p.K) + p.eps);
+  // each lane reads back only its own row: no cross-lane hand-over
+  epi_apply<T, EPI, 1>(p, tile, red, inv_rms, rg * 64, NORM, ein);
 }
 
 template <typename T, int MT>
 static int launch_reduce(int epi, const SkinnyParams& p, int ntiles, int S, int waves,
                          hipStream_t st) {
-  const dim3 grid((ntiles * MT + 3) / 4), blk(256);
+  constexpr int NRG = (MT * 16 + 63) / 64;
+  const dim3 grid((ntiles * NRG + 3) / 4), blk(256);
   const bool norm = p.eps > 0.f;
   switch (epi) {
     case EPI_PLAIN: wide_reduce_kernel<T, MT, EPI_PLAIN, false><<<grid, blk, 0, st>>>(p, ntiles, S, waves); return 0;

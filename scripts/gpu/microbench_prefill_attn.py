@@ -14,16 +14,35 @@ from agentic_traffic_testing_amd import ops  # noqa: E402
 from test_kernels_gpu import _make_paged, _tiles  # noqa: E402
 
 
+GRAPH = False
+
+
 def timeit(fn, iters=20, reps=3):
+    """us per call; with --graph the iters calls replay from one hipGraph (GPU time without
+    the host launch cost, which dominates the small burst shapes in eager mode)."""
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
+    g = None
+    if GRAPH:
+        g = torch.cuda.CUDAGraph()
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st), torch.cuda.graph(g, stream=st):
+            for _ in range(iters):
+                fn()
+        torch.cuda.current_stream().wait_stream(st)
+        g.replay()
+        torch.cuda.synchronize()
     res = []
     for _ in range(reps):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
-        for _ in range(iters):
-            fn()
+        if g is not None:
+            g.replay()
+        else:
+            for _ in range(iters):
+                fn()
         e.record()
         torch.cuda.synchronize()
         res.append(s.elapsed_time(e) / iters * 1000)
@@ -38,20 +57,33 @@ def main():
     ap.add_argument("--hq", type=int, nargs="+", default=[32, 64])
     ap.add_argument("--n", type=int, nargs="+", default=[0],
                     help="causal sequence lengths (0 = the default shape list)")
+    ap.add_argument("--multi", nargs="+", default=[],
+                    help="batched steps KV:Q:N - N sequences of Q new tokens over KV keys each "
+                         "(the cached burst: 617:17:5)")
+    ap.add_argument("--graph", action="store_true", help="time hipGraph replays")
     a = ap.parse_args()
+    global GRAPH
+    GRAPH = a.graph
     shapes = ((512, 512), (2600, 2600), (4096, 4096), (3000 + 700, 700), (8192, 8192))
     if a.n != [0]:
         shapes = tuple((n, n) for n in a.n)
+    steps = [[s] for s in shapes]
+    for m in a.multi:
+        kv_, q_, n_ = (int(v) for v in m.split(":"))
+        steps.append([(kv_, q_)] * n_)
+    if a.multi and a.n == [0]:
+        steps = steps[len(shapes):]
     dt = torch.bfloat16
     print("== prefill attention (us / TFLOP/s)")
     for hq, hkv in ((h, 8) for h in a.hq):
-        for kv, ql in shapes:
-            k, v, bt, kvlen, qstart, T = _make_paged([(kv, ql)], hkv, 16, dt)
+        for seqs in steps:
+            k, v, bt, kvlen, qstart, T = _make_paged(seqs, hkv, 16, dt)
             q = torch.randn(T, hq, 128, dtype=dt, device="cuda")
-            flops = 4 * 128 * hq * (ql * (kv - ql) + ql * (ql + 1) / 2)
-            row = f"Hq={hq:2d} kv={kv:5d} q={ql:5d} |"
+            flops = sum(4 * 128 * hq * (ql * (kv - ql) + ql * (ql + 1) / 2) for kv, ql in seqs)
+            kv, ql = seqs[0]
+            row = f"Hq={hq:2d} kv={kv:5d} q={ql:5d} x{len(seqs)} |"
             for impl in a.impls:
-                ts, to = _tiles([(kv, ql)], ops.prefill_tile_tokens(hq // hkv, impl))
+                ts, to = _tiles(seqs, ops.prefill_tile_tokens(hq // hkv, impl))
                 out = torch.empty_like(q)
                 t = timeit(lambda: ops.attention_prefill(q, k, v, bt, kvlen, qstart, ts, to,
                                                          0.088, out=out, impl=impl))
