@@ -67,6 +67,7 @@ def load_native(build_if_missing: bool = True) -> bool:
         _loaded = True
         _load_error = None
         torch.ops.atta.set_flash_waves(FLASH_WAVES)  # the host tiles follow this setting
+        torch.ops.atta.set_splitk_half(SPLITK_HALF)
         if WIDE_MAX_M <= SKINNY_MAX_M:  # wide kernel off: no <= 32-row call may take it
             torch.ops.atta.set_wide_min_rows(33, 33)
     except Exception as e:  # pragma: no cover - depends on environment
@@ -264,19 +265,61 @@ def set_flash_waves(nw: int) -> None:
 
 
 def attention_prefill(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, tile_seq,
-                      tile_qoff, scale, out=None, impl: str | None = None):
+                      tile_qoff, scale, out=None, impl: str | None = None,
+                      kv_splits: int | None = None):
     """Causal varlen prefill attention over the paged cache.  ``tile_seq`` / ``tile_qoff``
-    must come from tiles of ``prefill_tile_tokens(G, impl)`` tokens."""
+    must come from tiles of ``prefill_tile_tokens(G, impl)`` tokens.  ``kv_splits`` (flash
+    only): workgroups per (tile, KV head) over disjoint key ranges; None = ``flash_kv_splits``."""
     check_paged_args(k_cache, block_tables, seq_kvlen, what="attention_prefill")
     if not q.is_cuda:
         return ref.paged_attention(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart,
                                    scale, out=out)
     out = torch.empty_like(q) if out is None else out
-    fn = _native().flash_prefill if prefill_impl(block_tables.shape[1], impl) == "flash" else \
-        _native().attention_prefill
-    fn(out, q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, tile_seq, tile_qoff,
-       q.shape[1], k_cache.shape[1], scale)
+    if prefill_impl(block_tables.shape[1], impl) != "flash":
+        _native().attention_prefill(out, q, k_cache, v_cache, block_tables, seq_kvlen,
+                                    seq_qstart, tile_seq, tile_qoff, q.shape[1],
+                                    k_cache.shape[1], scale)
+        return out
+    pairs = tile_seq.shape[0] * k_cache.shape[1]
+    ns = flash_kv_splits(pairs) if kv_splits is None else int(kv_splits)
+    part = counters = None
+    if ns > 1:
+        part = torch.empty(pairs * ns * 16640, dtype=torch.float32, device=q.device)
+        counters = _flash_counters(q.device, pairs)
+    _native().flash_prefill(out, q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart,
+                            tile_seq, tile_qoff, q.shape[1], k_cache.shape[1], scale, ns, part,
+                            counters)
     return out
+
+
+# split-KV flash prefill: steps with few (tile, KV head) pairs over long cached prefixes (a short
+# suffix on a multi-thousand-token context leaves most CUs idle while each workgroup walks every
+# key block in turn) run up to FLASH_KV_SPLITS workgroups per pair over contiguous key ranges of
+# >= 8 blocks (decided per tile on the device) merged by the last arriver.  At the fan-out
+# bursts' ~600 keys it measured a wash (5 x 17 rows: 18.2 -> 16.5 us at 32 heads, 19.9 -> 21.2 at
+# 64; planning 10.1 -> 11.4 us), so those stay unsplit.  Long prefixes: 17 new rows over 4113
+# keys 91.3 -> 34.7 us, 33 over 8209 keys 188.6 -> 65.4 us at 4 splits
+# (profiles/r6_flash_split_kv.txt).
+# ATTA_FLASH_KV_SPLITS: 0 = auto, 1 = off, n = at most n
+FLASH_KV_SPLITS = int(os.environ.get("ATTA_FLASH_KV_SPLITS", "0"))
+_FLASH_COUNTERS: dict = {}
+
+
+def flash_kv_splits(pairs: int) -> int:
+    if FLASH_KV_SPLITS == 1 or pairs > 128:
+        return 1
+    cap = FLASH_KV_SPLITS if FLASH_KV_SPLITS > 1 else 8
+    return max(1, min(cap, 8, 256 // max(pairs, 1)))
+
+
+def _flash_counters(device, n: int) -> torch.Tensor:
+    """Zeroed arrival counters of the split-KV merge (re-armed by the kernel's last arrivers)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    c = _FLASH_COUNTERS.get(idx)
+    if c is None or c.numel() < n:
+        c = torch.zeros(max(n, 4096), dtype=torch.int32, device=device)
+        _FLASH_COUNTERS[idx] = c
+    return c
 
 
 def attention_decode(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, scale,
@@ -404,6 +447,19 @@ def auto_ksplit(tiles: int, K: int) -> int:
     while tiles * ks < 160 and K // (ks * 2) >= 2048:
         ks *= 2
     return ks
+
+# wide-kernel split-K slabs in bf16 (ATTA_SPLITK_HALF=1): half the slab traffic of the
+# qkv / o / down launches at 33-128 rows, each slice's partial rounded to bf16 once before the
+# fp32 slice-ordered sum
+SPLITK_HALF = int(os.environ.get("ATTA_SPLITK_HALF", "0"))
+
+
+def set_splitk_half(on: bool) -> None:
+    """bf16 (True) or fp32 (False) split-K slabs for the wide kernel's following launches."""
+    global SPLITK_HALF
+    SPLITK_HALF = int(bool(on))
+    _native().set_splitk_half(SPLITK_HALF)
+
 
 SPLITK_WS_FLOATS = 16 << 20  # 64 MiB: tiles x split x rows x 16 fp32 slots (mid-M splits)
 SPLITK_COUNTERS = 8192

@@ -167,12 +167,27 @@ void flash_prefill(at::Tensor out, const at::Tensor& q, const at::Tensor& k_cach
                    const at::Tensor& v_cache, const at::Tensor& block_tables,
                    const at::Tensor& seq_kvlen, const at::Tensor& seq_qstart,
                    const at::Tensor& tile_seq, const at::Tensor& tile_qoff, int64_t n_q_heads,
-                   int64_t n_kv_heads, double scale) {
+                   int64_t n_kv_heads, double scale, int64_t nsplit,
+                   const c10::optional<at::Tensor>& part,
+                   const c10::optional<at::Tensor>& counters) {
   check_dev(q, "q");
   TORCH_CHECK(block_tables.scalar_type() == at::kInt && seq_kvlen.scalar_type() == at::kInt &&
                   seq_qstart.scalar_type() == at::kInt && tile_seq.scalar_type() == at::kInt &&
                   tile_qoff.scalar_type() == at::kInt,
               "flash_prefill: metadata must be int32");
+  float* part_p = nullptr;
+  int* counters_p = nullptr;
+  if (nsplit > 1) {
+    TORCH_CHECK(part.has_value() && counters.has_value() &&
+                    part->scalar_type() == at::kFloat && counters->scalar_type() == at::kInt &&
+                    part->is_cuda() && counters->is_cuda() &&
+                    part->numel() * 4 >= tile_seq.size(0) * n_kv_heads * nsplit * 66560 &&
+                    counters->numel() >= tile_seq.size(0) * n_kv_heads,
+                "flash_prefill: split-KV needs fp32 partials [tiles * Hkv * nsplit * 16640] and "
+                "zeroed int32 counters [tiles * Hkv]");
+    part_p = part->data_ptr<float>();
+    counters_p = counters->data_ptr<int>();
+  }
   TORCH_CHECK(q.stride(-1) == 1 && out.stride(-1) == 1, "flash_prefill: last dim contiguous");
   TORCH_CHECK(q.scalar_type() == out.scalar_type() && k_cache.scalar_type() == q.scalar_type() &&
                   v_cache.scalar_type() == q.scalar_type(),
@@ -188,7 +203,8 @@ void flash_prefill(at::Tensor out, const at::Tensor& q, const at::Tensor& k_cach
                block_tables.data_ptr<int>(), seq_kvlen.data_ptr<int>(), seq_qstart.data_ptr<int>(),
                tile_seq.data_ptr<int>(), tile_qoff.data_ptr<int>(), tile_seq.size(0), n_q_heads,
                n_kv_heads, k_cache.size(3), k_cache.size(2), block_tables.stride(0), q.stride(0),
-               out.stride(0), static_cast<float>(scale), dtype_code(q), cur_stream()),
+               out.stride(0), static_cast<float>(scale), static_cast<int>(nsplit), part_p,
+               counters_p, dtype_code(q), cur_stream()),
            "flash_prefill");
 }
 
@@ -369,6 +385,7 @@ std::vector<int64_t> get_wide_min_rows() {
   atta_get_wide_min_rows(&m, &ms);
   return {m, ms};
 }
+void set_splitk_half(int64_t on) { atta_set_splitk_half(static_cast<int>(on)); }
 void set_midm_plan(int64_t bmt, int64_t ksplit) {
   atta_set_midm_plan(static_cast<int>(bmt), static_cast<int>(ksplit));
 }
@@ -841,6 +858,7 @@ TORCH_LIBRARY(atta, m) {
   m.def("set_wide_min_rows(int m, int m_silu) -> ()", &set_wide_min_rows);
   m.def("get_wide_min_rows() -> int[]", &get_wide_min_rows);
   m.def("set_midm_plan(int bmt, int ksplit) -> ()", &set_midm_plan);
+  m.def("set_splitk_half(int on) -> ()", &set_splitk_half);
   m.def("midm_plan(int M, int ntiles, int K, int epi, int ws_floats) -> int[]", &midm_plan);
   m.def("set_flash_waves(int nw) -> ()", &set_flash_waves);
   m.def("prefill_gemm_config(int schedule, int group_m, int ablate=0) -> ()", &prefill_gemm_config);
@@ -860,7 +878,8 @@ TORCH_LIBRARY(atta, m) {
   m.def(
       "flash_prefill(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
       "Tensor block_tables, Tensor seq_kvlen, Tensor seq_qstart, Tensor tile_seq, "
-      "Tensor tile_qoff, int n_q_heads, int n_kv_heads, float scale) -> ()");
+      "Tensor tile_qoff, int n_q_heads, int n_kv_heads, float scale, int nsplit=1, "
+      "Tensor(b!)? part=None, Tensor(c!)? counters=None) -> ()");
   m.def(
       "attention_decode(Tensor(a!) out, Tensor(b!) part_out, Tensor(c!) part_lse, Tensor q, "
       "Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor seq_kvlen, "

@@ -82,7 +82,18 @@ struct FlashParams {
   int64_t q_stride, out_stride;
   int bt_stride, n_kv_heads, bs_shift;
   float scale_log2;
+  // split-KV (few tiles over long cached prefixes: the cached burst / planning steps): up to
+  // nsplit workgroups per (tile, KV head) each walk a contiguous range of key blocks and
+  // publish (O, m, l) partials; the last to arrive merges them (device-scope hand-over)
+  int nsplit;
+  float* part;    // [tile, Hkv, nsplit] slots of kPartBytes
+  int* counters;  // [tile * Hkv], zero between launches (the last arriver re-arms)
 };
+// one split's partial: 128 columns x 128 fp32 O values, then 128 (m, l) pairs
+constexpr uint32_t kPartOBytes = 128 * kD * 4;
+constexpr uint32_t kPartBytes = kPartOBytes + 128 * 8;
+constexpr int kMaxSplit = 8;
+constexpr int kSplitBlocks = 8;  // 512 keys
 
 // two floats -> one packed 16-bit pair.  bf16: a single v_cvt_pk_bf16_f32 (RNE); element-wise
 // conversion compiled to 2 converts + shift + or per pair, 64 VALU per block per wave.
@@ -130,7 +141,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_prefill_kernel(FlashPar
   // emitted in token order per sequence.
   const int bid = static_cast<int>(blockIdx.x);
   const int hk = bid % p.n_kv_heads;
-  const int tile = p.num_tiles - 1 - bid / p.n_kv_heads;
+  const int rest = bid / p.n_kv_heads;
+  const int sp = rest % p.nsplit;  // key-range split of this workgroup
+  const int tile = p.num_tiles - 1 - rest / p.nsplit;
   const int s = p.tile_seq[tile];
   const int qoff = p.tile_qoff[tile];
   const int kvlen = p.seq_kvlen[s];  // >= wg_end: every key this workgroup reads is below it
@@ -154,6 +167,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_prefill_kernel(FlashPar
   const int w_last_tok = min(qoff + (wid + 1) * kTokPerWave, qlen) - 1;
   const int w_end = w_last_tok >= qoff + wid * kTokPerWave ? ctx0 + w_last_tok + 1 : 0;
   const int w_first = qoff + wid * kTokPerWave;  // first token: fully visible below ctx0+w_first+1
+  // this tile's splits: >= kSplitBlocks key blocks each (a split pays a publish + merge chain
+  // of ~2 us: at the cached burst's ~10 blocks per tile it measured a wash), workgroups past
+  // them exit before any barrier
+  const int ns = max(1, min(p.nsplit, nblocks / kSplitBlocks));
+  if (sp >= ns) return;
+  const int kb0 = sp * nblocks / ns, kb1 = (sp + 1) * nblocks / ns;
 
   // ---- block table slice -> LDS -------------------------------------------------------
   const int npages = min((wg_end + BS - 1) >> p.bs_shift, kBtLds);
@@ -259,15 +278,15 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_prefill_kernel(FlashPar
     for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
   float m_run = kNegInf, l_run = 0.f;
 
-  if (nblocks > 0) {
-    load_block(0);
-    store_block(0, 0);
+  if (kb0 < kb1) {
+    load_block(kb0);
+    store_block(0, kb0);
   }
   __syncthreads();
 
-  for (int kb = 0; kb < nblocks; ++kb) {
-    const int buf = kb & 1;
-    const bool more = kb + 1 < nblocks;
+  for (int kb = kb0; kb < kb1; ++kb) {
+    const int buf = (kb - kb0) & 1;
+    const bool more = kb + 1 < kb1;
     const int k0 = kb * kKB;
     bool issued = false;
     if (k0 < w_end) {  // wave-uniform: the wave has visible keys in this block
@@ -376,6 +395,79 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_prefill_kernel(FlashPar
     __syncthreads();
   }
 
+  if (ns > 1) {
+    // ---- split-KV hand-over: publish (O, m, l) with device-scope stores, count arrivals; the
+    // last workgroup of the tile merges every split's partial into its own registers
+    __shared__ int fl_last;
+    const auto rw = dev_rsrc(p.part);
+    const int pair = tile * p.n_kv_heads + hk;
+    const uint32_t base = static_cast<uint32_t>(pair * p.nsplit) * kPartBytes;
+    const int col = wid * 32 + r;
+    // lane (col r, half h): O^T element (dt, i) is d = 32 dt + 8 (i >> 2) + 4 h + (i & 3)
+    if (c_valid) {
+      const uint32_t mine = base + static_cast<uint32_t>(sp) * kPartBytes;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          dev_store16(rw, mine + (col * kD + 32 * dt + 8 * g + 4 * h) * 4,
+                      u32x4{__float_as_uint(o[dt][4 * g]), __float_as_uint(o[dt][4 * g + 1]),
+                            __float_as_uint(o[dt][4 * g + 2]), __float_as_uint(o[dt][4 * g + 3])});
+      if (h == 0) {
+        dev_store4(rw, mine + kPartOBytes + col * 8, m_run);
+        dev_store4(rw, mine + kPartOBytes + col * 8 + 4, l_run);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores acknowledged
+    __syncthreads();
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(p.counters + pair, 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      fl_last = old == ns - 1;
+    }
+    __syncthreads();
+    if (!fl_last) return;  // block-uniform
+    if (tid == 0)
+      __hip_atomic_store(p.counters + pair, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c_valid) {
+      float mq[kMaxSplit], lq[kMaxSplit];  // fully unrolled: registers, not scratch
+      float M = m_run;
+#pragma unroll
+      for (int q = 0; q < kMaxSplit; ++q) {
+        mq[q] = kNegInf;
+        lq[q] = 0.f;
+        if (q >= ns || q == sp) continue;
+        const uint32_t at = base + static_cast<uint32_t>(q) * kPartBytes + kPartOBytes + col * 8;
+        mq[q] = dev_load4(rw, at);
+        lq[q] = dev_load4(rw, at + 4);
+        M = fmaxf(M, mq[q]);
+      }
+      // every split's O and l are relative to its own running max (log2 units)
+      const float Mu = M == kNegInf ? 0.f : M;
+      const float wself = __builtin_amdgcn_exp2f(m_run - Mu);
+      l_run *= wself;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[dt][i] *= wself;
+#pragma unroll
+      for (int q = 0; q < kMaxSplit; ++q) {
+        if (q >= ns || q == sp) continue;
+        const float wq = __builtin_amdgcn_exp2f(mq[q] - Mu);
+        l_run += wq * lq[q];
+        const uint32_t at = base + static_cast<uint32_t>(q) * kPartBytes;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const u32x4 v = dev_load16(rw, at + (col * kD + 32 * dt + 8 * g + 4 * h) * 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[dt][4 * g + j] += wq * __uint_as_float(v[j]);
+          }
+      }
+    }
+  }
+
   // ---- epilogue: O = O^T / l, lane (col r, half h) holds d = 32 dt + (i & 3) + 8 (i >> 2) + 4 h
   if (c_valid) {
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
@@ -425,8 +517,8 @@ int atta_flash_prefill(void* out, const void* q, const void* k_cache, const void
                        const int* block_tables, const int* seq_kvlen, const int* seq_qstart,
                        const int* tile_seq, const int* tile_qoff, int num_tiles, int n_q_heads,
                        int n_kv_heads, int head_dim, int block_size, int bt_stride,
-                       int64_t q_stride, int64_t out_stride, float scale, int dtype,
-                       hipStream_t stream) {
+                       int64_t q_stride, int64_t out_stride, float scale, int nsplit,
+                       float* part, int* counters, int dtype, hipStream_t stream) {
   const int G = n_q_heads / n_kv_heads;
   int shift = 0;
   while ((1 << shift) < block_size) ++shift;
@@ -453,7 +545,14 @@ int atta_flash_prefill(void* out, const void* q, const void* k_cache, const void
   prm.n_kv_heads = n_kv_heads;
   prm.bs_shift = shift;
   prm.scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid(num_tiles * n_kv_heads);
+  if (nsplit < 1 || nsplit > fp::kMaxSplit) return -1;
+  if (nsplit > 1 && (part == nullptr || counters == nullptr)) return -2;
+  // 32-bit byte offsets of the device-scope partial stores
+  if (static_cast<int64_t>(num_tiles) * n_kv_heads * nsplit * fp::kPartBytes > 0x7FFFFFFF) return -1;
+  prm.nsplit = nsplit;
+  prm.part = part;
+  prm.counters = counters;
+  dim3 grid(num_tiles * n_kv_heads * nsplit);
   const int rc = dtype == 0 ? fp::launch<__bf16>(G, grid, stream, prm)
                             : fp::launch<_Float16>(G, grid, stream, prm);
   if (rc) return rc;

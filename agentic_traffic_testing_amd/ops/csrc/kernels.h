@@ -39,8 +39,8 @@ int atta_flash_prefill(void* out, const void* q, const void* k_cache, const void
                        const int* block_tables, const int* seq_kvlen, const int* seq_qstart,
                        const int* tile_seq, const int* tile_qoff, int num_tiles, int n_q_heads,
                        int n_kv_heads, int head_dim, int block_size, int bt_stride,
-                       int64_t q_stride, int64_t out_stride, float scale, int dtype,
-                       hipStream_t stream);
+                       int64_t q_stride, int64_t out_stride, float scale, int nsplit,
+                       float* part, int* counters, int dtype, hipStream_t stream);
 
 int atta_attention_decode(void* out, float* part_out, float* part_lse, const void* q,
                           const void* k_cache, const void* v_cache, const int* block_tables,
@@ -155,6 +155,7 @@ void atta_get_wide_min_rows(int* m, int* m_silu);
 // mid-M GEMM (midm.hip): the next launch's plan (row-block height bmt x 16, K slices; 0 =
 // planned) and the plan the library would pick for a shape
 void atta_set_midm_plan(int bmt, int ksplit);
+void atta_set_splitk_half(int on);
 int atta_midm_plan(int M, int ntiles, int K, int epi, int64_t ws_floats, int* bmt, int* ksplit);
 void atta_set_flash_waves(int nw);
 int atta_prefill_gemm_config(int schedule, int group_m, int ablate);

@@ -91,6 +91,9 @@ struct SkinnyParams {
   int ksplit;
   float* sk_ws;
   int* sk_counters;
+  // wide / mid-M split-K slabs in bf16 instead of fp32 (half the slab write + reduce read
+  // traffic; each slice's partial rounded once before the fp32 slice-ordered sum)
+  int sk_half;
   // optional per-workgroup timeline (ops.set_gemv_trace): [start, end] on the 100 MHz wall
   // clock per workgroup of the grid (gridDim.y == 1 launches only)
   unsigned long long* wg_trace;

@@ -499,11 +499,21 @@ __global__ __launch_bounds__(WAVES * 64) void wide_kernel(SkinnyParams p, int nt
       for (int j = 0; j < (R > 64 ? 2 : 1); ++j) {
         const int row = lane + 64 * j;
         if (row < R && row < p.M) {
-          float* dst = p.sk_ws + ((static_cast<int64_t>(tile) * S + ks) * R + row) * 16;
+          const int64_t at = ((static_cast<int64_t>(tile) * S + ks) * R + row) * 16;
+          if (p.sk_half) {
+            uint16_t o[2][8];
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            reinterpret_cast<f32x4*>(dst)[q] =
-                f32x4{red[row][4 * q], red[row][4 * q + 1], red[row][4 * q + 2], red[row][4 * q + 3]};
+            for (int n = 0; n < 16; ++n) o[n >> 3][n & 7] = from_f32<__bf16>(red[row][n]);
+            u32x4* dst = reinterpret_cast<u32x4*>(reinterpret_cast<uint16_t*>(p.sk_ws) + at);
+            dst[0] = pack8(o[0]);
+            dst[1] = pack8(o[1]);
+          } else {
+            float* dst = p.sk_ws + at;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              reinterpret_cast<f32x4*>(dst)[q] =
+                  f32x4{red[row][4 * q], red[row][4 * q + 1], red[row][4 * q + 2], red[row][4 * q + 3]};
+          }
         }
       }
     }

@@ -37,10 +37,21 @@ __global__ __launch_bounds__(256) void wide_reduce_kernel(SkinnyParams p, int nt
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int ks = min(k0 + u, S - 1);
-      const f32x4* src =
-          reinterpret_cast<const f32x4*>(p.sk_ws + ((static_cast<int64_t>(tile) * S + ks) * R + rc) * 16);
+      const int64_t at = ((static_cast<int64_t>(tile) * S + ks) * R + rc) * 16;
+      if (p.sk_half) {  // bf16 slab: 16 values in two 16-B loads
+        const u32x4* src = reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(p.sk_ws) + at);
+        const u32x4 h0 = src[0], h1 = src[1];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) part[u][q] = src[q];
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t w0 = (q < 2 ? h0 : h1)[(q & 1) * 2], w1 = (q < 2 ? h0 : h1)[(q & 1) * 2 + 1];
+          part[u][q] = f32x4{__uint_as_float(w0 << 16), __uint_as_float(w0 & 0xffff0000u),
+                             __uint_as_float(w1 << 16), __uint_as_float(w1 & 0xffff0000u)};
+        }
+      } else {
+        const f32x4* src = reinterpret_cast<const f32x4*>(p.sk_ws + at);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) part[u][q] = src[q];
+      }
       if constexpr (NORM)
         sp[u] = p.sk_ws[static_cast<int64_t>(ntiles) * S * R * 16 +
                         (static_cast<int64_t>(cb) * S + ks) * R + rc];
@@ -181,6 +192,10 @@ using namespace atta;
 // pre-shuffled 16-bit, y / epilogue fields, eps, M, N, K).  ntiles: 16-column tiles (N / 16;
 // SiLU: inter / 8).  waves / ksplit 0 = planned here.  Returns 0, -1 (unsupported shape) or
 // -2 (split-K workspace missing / too small).
+// split-K slab precision of the wide kernel (atta_set_splitk_half): 0 fp32, 1 bf16
+static int g_sk_half = 0;
+void atta_set_splitk_half(int on) { g_sk_half = on ? 1 : 0; }
+
 int atta_wide_launch(SkinnyParams& p, int epi, int ntiles, int waves, int ksplit, int dtype,
                      const float* sk_ws, int* sk_counters, int64_t ws_floats, int n_counters,
                      hipStream_t stream) {
@@ -212,6 +227,7 @@ int atta_wide_launch(SkinnyParams& p, int epi, int ntiles, int waves, int ksplit
     if (sk_ws == nullptr) return -2;
     p.sk_ws = const_cast<float*>(sk_ws);
     p.sk_counters = sk_counters;
+    p.sk_half = g_sk_half;
   }
   (void)n_counters;
   p.ksplit = ksplit;

@@ -133,6 +133,31 @@ def _tiles(seqs, tile):
             torch.tensor(to, dtype=torch.int32, device="cuda"))
 
 
+@pytest.mark.parametrize("splits", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (24, 8)])
+def test_flash_prefill_split_kv(splits, hq, hkv):
+    """Split-KV flash prefill (up to `splits` workgroups per (tile, KV head) over contiguous key
+    ranges of >= 8 blocks, merged by the last arriver): the cached burst (5 x 17 new tokens over
+    617 keys), a planning step over a 176-token prefix, a short fresh prompt, a chunk after a
+    prefix, a full causal prompt and short suffixes over 2-4k cached keys (the split cases) -
+    against the fp32 reference, run twice (the arrival counters re-arm)."""
+    torch.manual_seed(9)
+    dt = torch.bfloat16
+    seqs = [(617, 17)] * 5 + [(193, 17), (17, 17), (300, 77), (640, 640), (4113, 17),
+                                (2100, 40)]
+    k, v, bt, kvlen, qstart, T = _make_paged(seqs, hkv, 16, dt)
+    q = torch.randn(T, hq, 128, dtype=dt, device="cuda")
+    ts, to = _tiles(seqs, ops.prefill_tile_tokens(hq // hkv, "flash"))
+    scale = 1 / math.sqrt(128)
+    exp = ref.paged_attention(q, k, v, bt.clamp(min=0), kvlen, qstart, scale)
+    for _ in range(2):
+        got = ops.attention_prefill(q, k, v, bt, kvlen, qstart, ts, to, scale, impl="flash",
+                                    kv_splits=splits)
+        close(got, exp, 1.5e-2, 2e-2)
+    assert int(ops._FLASH_COUNTERS.get(torch.cuda.current_device(),
+                                       torch.zeros(1, device="cuda")).abs().sum()) == 0
+
+
 @pytest.mark.parametrize("impl", ["flash", "v1"])
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 1), (4, 1), (16, 16), (24, 8)])

@@ -240,3 +240,25 @@ def test_wide_fp8_matches_skinny_at_the_seam():
     a = ops.linear(x[:32].contiguous(), wq, w_scale=s)
     b = ops.linear(x, wq, w_scale=s)
     close(b[:32], a, 2e-2, 1e-2)
+
+
+def test_wide_splitk_half_slabs():
+    """ATTA_SPLITK_HALF / ops.set_splitk_half: bf16 split-K slabs (half the slab traffic,
+    3-10 % per layer at 85-128 rows) round each slice's partial once, so their error vs the fp32
+    oracle grows with the partials' magnitude, not the result's (off by default: a cancelling
+    row can lose ~1 % relative).  Checked here against the fp32-slab kernel's own error."""
+    torch.manual_seed(50)
+    dt = torch.bfloat16
+    x = torch.randn(85, 4096, dtype=dt, device="cuda")
+    w = torch.randn(4096, 4096, dtype=dt, device="cuda") * 0.02
+    wp = ops.preshuffle(w)
+    exp = x.float() @ w.float().t()
+    errs = {}
+    try:
+        for half in (False, True):
+            ops.set_splitk_half(half)
+            ops.set_wide_plan(8, 4)
+            errs[half] = float((ops.linear(x, wp, preshuffled=True).float() - exp).abs().max())
+    finally:
+        ops.set_splitk_half(False)
+    assert errs[True] <= 4 * errs[False] + 2e-2, errs
