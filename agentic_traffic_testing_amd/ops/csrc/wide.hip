@@ -150,6 +150,11 @@ static void plan(int ntiles, int K, int M, bool norm, bool w8, int& waves, int& 
   // cost-model knobs (env overrides for A/B runs; read once)
   static const double kXDiv = env_or("ATTA_WIDE_PLAN_XDIV", 6.0);
   static const double kRed = env_or("ATTA_WIDE_PLAN_RED_US", 1.0);
+  // split-K slab bytes per us (written by the slices, read back by the reduce): 2e6 refit to
+  // the round-6 graph-mode sweep of every (waves, split) plan of qkv / o / down at 50-105
+  // rows (best-per-shape sum 374.6 us; the planner's picks 387.5 us at 5e6, 378.9 at 2e6:
+  // down moves from 8 x 8 to 4 x 4)
+  static const double kSlabBpus = env_or("ATTA_WIDE_PLAN_SLAB_BPUS", 2e6);
   const int mpad = ((M + 15) / 16) * 16;
   const int nch = K / kKC;
   double best = 1e30;
@@ -171,7 +176,7 @@ static void plan(int ntiles, int K, int M, bool norm, bool w8, int& waves, int& 
         // (profiles/r5_wide_tiles_per_wave_negative.txt: 626 vs 640 us over 20 shapes)
         const double slab = static_cast<double>(ntiles) * s * mpad * 64.0;
         const double t = rounds * (bytes / kBpus * (1.0 + 0.5 * idle) + 1.5) +
-                         (s > 1 ? kRed + slab / 5e6 : 0.0);
+                         (s > 1 ? kRed + slab / kSlabBpus : 0.0);
         if (t < best - 1e-9) {
           best = t;
           waves = w;
