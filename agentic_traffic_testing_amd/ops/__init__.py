@@ -68,6 +68,7 @@ def load_native(build_if_missing: bool = True) -> bool:
         _load_error = None
         torch.ops.atta.set_flash_waves(FLASH_WAVES)  # the host tiles follow this setting
         torch.ops.atta.set_splitk_half(SPLITK_HALF)
+        torch.ops.atta.set_flash_split_blocks(FLASH_SPLIT_BLOCKS)
         if WIDE_MAX_M <= SKINNY_MAX_M:  # wide kernel off: no <= 32-row call may take it
             torch.ops.atta.set_wide_min_rows(33, 33)
     except Exception as e:  # pragma: no cover - depends on environment
@@ -302,6 +303,8 @@ def attention_prefill(q, k_cache, v_cache, block_tables, seq_kvlen, seq_qstart, 
 # (profiles/r6_flash_split_kv.txt).
 # ATTA_FLASH_KV_SPLITS: 0 = auto, 1 = off, n = at most n
 FLASH_KV_SPLITS = int(os.environ.get("ATTA_FLASH_KV_SPLITS", "0"))
+# fewest 64-key blocks per split (ATTA_FLASH_SPLIT_BLOCKS; a tile splits nblocks // this ways)
+FLASH_SPLIT_BLOCKS = int(os.environ.get("ATTA_FLASH_SPLIT_BLOCKS", "8"))
 _FLASH_COUNTERS: dict = {}
 
 

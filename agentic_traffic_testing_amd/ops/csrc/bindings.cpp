@@ -386,6 +386,7 @@ std::vector<int64_t> get_wide_min_rows() {
   return {m, ms};
 }
 void set_splitk_half(int64_t on) { atta_set_splitk_half(static_cast<int>(on)); }
+void set_flash_split_blocks(int64_t nb) { atta_set_flash_split_blocks(static_cast<int>(nb)); }
 void set_midm_plan(int64_t bmt, int64_t ksplit) {
   atta_set_midm_plan(static_cast<int>(bmt), static_cast<int>(ksplit));
 }
@@ -859,6 +860,7 @@ TORCH_LIBRARY(atta, m) {
   m.def("get_wide_min_rows() -> int[]", &get_wide_min_rows);
   m.def("set_midm_plan(int bmt, int ksplit) -> ()", &set_midm_plan);
   m.def("set_splitk_half(int on) -> ()", &set_splitk_half);
+  m.def("set_flash_split_blocks(int nb) -> ()", &set_flash_split_blocks);
   m.def("midm_plan(int M, int ntiles, int K, int epi, int ws_floats) -> int[]", &midm_plan);
   m.def("set_flash_waves(int nw) -> ()", &set_flash_waves);
   m.def("prefill_gemm_config(int schedule, int group_m, int ablate=0) -> ()", &prefill_gemm_config);

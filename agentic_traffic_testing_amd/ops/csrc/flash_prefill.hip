@@ -86,6 +86,7 @@ struct FlashParams {
   // nsplit workgroups per (tile, KV head) each walk a contiguous range of key blocks and
   // publish (O, m, l) partials; the last to arrive merges them (device-scope hand-over)
   int nsplit;
+  int split_blocks;  // key blocks per split at least (atta_set_flash_split_blocks)
   float* part;    // [tile, Hkv, nsplit] slots of kPartBytes
   int* counters;  // [tile * Hkv], zero between launches (the last arriver re-arms)
 };
@@ -93,7 +94,7 @@ struct FlashParams {
 constexpr uint32_t kPartOBytes = 128 * kD * 4;
 constexpr uint32_t kPartBytes = kPartOBytes + 128 * 8;
 constexpr int kMaxSplit = 8;
-constexpr int kSplitBlocks = 8;  // 512 keys
+constexpr int kSplitBlocks = 8;  // 512 keys: the default of split_blocks
 
 // two floats -> one packed 16-bit pair.  bf16: a single v_cvt_pk_bf16_f32 (RNE); element-wise
 // conversion compiled to 2 converts + shift + or per pair, 64 VALU per block per wave.
@@ -170,7 +171,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_prefill_kernel(FlashPar
   // this tile's splits: >= kSplitBlocks key blocks each (a split pays a publish + merge chain
   // of ~2 us: at the cached burst's ~10 blocks per tile it measured a wash), workgroups past
   // them exit before any barrier
-  const int ns = max(1, min(p.nsplit, nblocks / kSplitBlocks));
+  const int ns = max(1, min(p.nsplit, nblocks / p.split_blocks));
   if (sp >= ns) return;
   const int kb0 = sp * nblocks / ns, kb1 = (sp + 1) * nblocks / ns;
 
@@ -512,6 +513,8 @@ static int launch(int G, dim3 grid, hipStream_t st, const FlashParams& p) {
 using namespace atta;
 
 void atta_set_flash_waves(int nw) { fp::g_flash_waves = nw == 8 ? 8 : 4; }
+static int g_split_blocks = fp::kSplitBlocks;
+void atta_set_flash_split_blocks(int nb) { g_split_blocks = nb < 1 ? 1 : nb; }
 
 int atta_flash_prefill(void* out, const void* q, const void* k_cache, const void* v_cache,
                        const int* block_tables, const int* seq_kvlen, const int* seq_qstart,
@@ -550,6 +553,7 @@ int atta_flash_prefill(void* out, const void* q, const void* k_cache, const void
   // 32-bit byte offsets of the device-scope partial stores
   if (static_cast<int64_t>(num_tiles) * n_kv_heads * nsplit * fp::kPartBytes > 0x7FFFFFFF) return -1;
   prm.nsplit = nsplit;
+  prm.split_blocks = g_split_blocks;
   prm.part = part;
   prm.counters = counters;
   dim3 grid(num_tiles * n_kv_heads * nsplit);

@@ -156,6 +156,7 @@ void atta_get_wide_min_rows(int* m, int* m_silu);
 // planned) and the plan the library would pick for a shape
 void atta_set_midm_plan(int bmt, int ksplit);
 void atta_set_splitk_half(int on);
+void atta_set_flash_split_blocks(int nb);
 int atta_midm_plan(int M, int ntiles, int K, int epi, int64_t ws_floats, int* bmt, int* ksplit);
 void atta_set_flash_waves(int nw);
 int atta_prefill_gemm_config(int schedule, int group_m, int ablate);

@@ -191,8 +191,10 @@ def test_flash_prefill_8_waves_bit_identical(dtype, hq, hkv):
         for nw in (4, 8):
             ops.set_flash_waves(nw)
             ts, to = _tiles(seqs, ops.prefill_tile_tokens(hq // hkv, "flash"))
+            # unsplit: the 4- and 8-wave tiles differ in size, so an automatic split-KV plan
+            # (per tile count) would sum different key ranges (test_flash_prefill_split_kv)
             outs[nw] = ops.attention_prefill(q, k, v, bt, kvlen, qstart, ts, to, scale,
-                                             impl="flash")
+                                             impl="flash", kv_splits=1)
     finally:
         ops.set_flash_waves(int(os.environ.get("ATTA_FLASH_WAVES", "4")))
     assert torch.equal(outs[4], outs[8])
