@@ -522,9 +522,10 @@ class LlamaModel:
     # vs 47.4 at 128; 70B 106 vs 117 at 33 rows, 123 vs 118 at 64).  qkv / o / down keep the
     # W8 builds to 128 rows (1.14-1.9x at <= 96 rows, 0.93-0.97x at 128 on the 70B shapes)
     FP8_GATE_UP_WIDE_MAX = {4096: 112, 8192: 48}
-    # and the whole fused step: 70B fp8 prefill 33 / 76 / 128 rows 15.4 / 21.4 / 24.3 ms fused
-    # vs 20.6 / 22.4 / 23.3 on the library chain (profiles/r6_70b_fp8_planning_prefill.txt)
-    FP8_FUSED_MAX_ROWS = {8192: 112}
+    # and the whole fused step: 70B fp8 prefill 33 / 76 / 112 / 128 rows 15.4 / 21.4 / 23.8 /
+    # 24.3 ms fused vs 20.6 / 22.4 / 23.2 / 23.3 on the library chain
+    # (profiles/r6_70b_fp8_planning_prefill.txt)
+    FP8_FUSED_MAX_ROWS = {8192: 96}
 
     def _fp8_fused_max(self) -> int:
         if self.tp_size > 1:

@@ -153,7 +153,8 @@ static void plan(int ntiles, int K, int M, bool norm, bool w8, int& waves, int& 
   // split-K slab bytes per us (written by the slices, read back by the reduce): 2e6 refit to
   // the round-6 graph-mode sweep of every (waves, split) plan of qkv / o / down at 50-105
   // rows (best-per-shape sum 374.6 us; the planner's picks 387.5 us at 5e6, 378.9 at 2e6:
-  // down moves from 8 x 8 to 4 x 4)
+  // down moves from 8 x 8 to 4 x 4).  The fp8-weight (W8) plans keep 5e6: at the 70B shapes
+  // 2e6 chose fewer splits and the 76-row prefill went 21.4 -> 22.2 ms
   static const double kSlabBpus = env_or("ATTA_WIDE_PLAN_SLAB_BPUS", 2e6);
   const int mpad = ((M + 15) / 16) * 16;
   const int nch = K / kKC;
@@ -176,7 +177,7 @@ static void plan(int ntiles, int K, int M, bool norm, bool w8, int& waves, int& 
         // (profiles/r5_wide_tiles_per_wave_negative.txt: 626 vs 640 us over 20 shapes)
         const double slab = static_cast<double>(ntiles) * s * mpad * 64.0;
         const double t = rounds * (bytes / kBpus * (1.0 + 0.5 * idle) + 1.5) +
-                         (s > 1 ? kRed + slab / kSlabBpus : 0.0);
+                         (s > 1 ? kRed + slab / (w8 ? 5e6 : kSlabBpus) : 0.0);
         if (t < best - 1e-9) {
           best = t;
           waves = w;
