@@ -156,6 +156,10 @@ static void plan(int ntiles, int K, int M, bool norm, bool w8, int& waves, int& 
   // down moves from 8 x 8 to 4 x 4).  The fp8-weight (W8) plans keep 5e6: at the 70B shapes
   // 2e6 chose fewer splits and the 76-row prefill went 21.4 -> 22.2 ms
   static const double kSlabBpus = env_or("ATTA_WIDE_PLAN_SLAB_BPUS", 2e6);
+  // a wave count the 16-bit plans skip (A/B runs; 0 = none).  gate_up's 7 x 1 (256 workgroups)
+  // loses to 8 x 1 in isolated back-to-back replays but wins in situ on the fan-out bench
+  // (profiles/r6_gate_up_7v8_waves.txt), so nothing is skipped by default
+  static const int kSkipW = static_cast<int>(env_or("ATTA_WIDE_PLAN_SKIP_WAVES", 0.0));
   const int mpad = ((M + 15) / 16) * 16;
   const int nch = K / kKC;
   double best = 1e30;
@@ -163,6 +167,7 @@ static void plan(int ntiles, int K, int M, bool norm, bool w8, int& waves, int& 
   for (int tp = 1; tp <= 1; ++tp) {  // tpw 2: measured slower, not built (wide.h launch_t)
     for (int wi = 0; wi < 4; ++wi) {
       const int w = ws[wi];
+      if (!w8 && w == kSkipW) continue;
       if (norm && !norm_fits(w, (M + 15) / 16, tp)) continue;  // see launch_epi
       if (tp == 2 && !tpw2_built(w)) continue;
       const int tb = w * tp;
