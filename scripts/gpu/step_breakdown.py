@@ -1,7 +1,8 @@
 """Kernel-time breakdown of one cached-burst prefill step from a rocprofv3 kernel-trace CSV
 directory: the contiguous run of dispatches around the first wide small-M GEMM launch of at
 least ``--mt-min`` 16-row blocks (the 50-105-row bursts of the fan-out bench), from the embed
-kernel before it to the first decode-step kernel after it.  Prints, per kernel class, the
+kernel before it to the first decode-step kernel after it (start-up warm-up launches, which
+have no embed kernel before them, are skipped).  Prints, per kernel class, the
 launches and summed GPU time, plus the span's idle time.
 
     python scripts/gpu/step_breakdown.py DIR [--mt-min 4] [--nth 0]
@@ -52,10 +53,22 @@ for i in starts[1:]:
     else:
         cur.append(i)
 steps.append(cur)
+
+
+def embed_before(i):
+    while i > 0 and "embed_kernel" not in raw[i][2]:
+        i -= 1
+    return i
+
+
+# engine start-up warm-up launches (ops.warm_wide_kernels, EngineConfig.startup_warmup) have no
+# embed kernel right before them: only groups within 2 ms of an embed launch are prefill steps
+steps = [g for g in steps if raw[g[0]][0] - raw[embed_before(g[0])][1] < 2_000_000]
+if not steps:
+    print("no prefill step with a wide launch of MT >=", mt_min)
+    sys.exit(0)
 sel = steps[min(nth, len(steps) - 1)]
-lo = sel[0]
-while lo > 0 and "embed_kernel" not in raw[lo][2]:
-    lo -= 1
+lo = embed_before(sel[0])
 hi = sel[-1]
 while hi + 1 < len(raw) and cls(raw[hi + 1][2]) not in ("skinny_kernel", "embed_kernel") and \
         raw[hi + 1][0] - raw[hi][1] < 1_000_000:
